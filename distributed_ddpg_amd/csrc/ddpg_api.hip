@@ -1,0 +1,1333 @@
+// C-ABI implementation of the MI355X-native DDPG learner hot path.
+// See include/ddpg_hip.h for the boundary and the reference interfaces each
+// entry point replaces; DESIGN.md for the data layout and kernel list.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ddpg_hip.h"
+#include "gemm_f32.h"
+#include "kernels.h"
+#include "sampler.h"
+
+using namespace ddpg;
+
+// ====================================================================== errors
+static thread_local std::string g_err;
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw DdpgError(DDPG_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));    \
+  } while (0)
+
+struct DdpgError {
+  int code;
+  std::string msg;
+  DdpgError(int c, std::string m) : code(c), msg(std::move(m)) {}
+};
+
+static DdpgError einval(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  return DdpgError(DDPG_EINVAL, buf);
+}
+
+static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+// ====================================================================== layout
+// Flat parameter layout: actor tensors then critic tensors, each tensor
+// starting on a 64-float (256 B) boundary.  theta / target / m / v / grad all
+// share it, so Adam and the soft update are single coalesced passes.
+struct Tensor {
+  int rows, cols;  // cols == 1 and rows == n for vectors
+  size_t off;      // float offset in the flat buffer
+  size_t count() const { return (size_t)rows * cols; }
+};
+
+enum { AW1, AB1, AW2, AB2, AW3, NA };
+enum { CWS, CBS, CWA, CBA, CWH, CBH, CWO, CBO, NC };
+
+struct Layout {
+  Tensor a[NA], c[NC];
+  size_t actor_begin, actor_end, critic_begin, critic_end, total;
+  void build(int S, int A, int H1, int H2) {
+    size_t off = 0;
+    auto place = [&](Tensor& t, int r, int c) {
+      t.rows = r;
+      t.cols = c;
+      t.off = off;
+      off += ((size_t)r * c + 63) / 64 * 64;
+    };
+    actor_begin = 0;
+    place(a[AW1], S, H1);
+    place(a[AB1], H1, 1);
+    place(a[AW2], H1, H2);
+    place(a[AB2], H2, 1);
+    place(a[AW3], H2, A);
+    actor_end = critic_begin = off;
+    place(c[CWS], S, H1);
+    place(c[CBS], H1, 1);
+    place(c[CWA], A, H1);
+    place(c[CBA], H1, 1);
+    place(c[CWH], 2 * H1, H2);
+    place(c[CBH], H2, 1);
+    place(c[CWO], H2, 1);
+    place(c[CBO], 1, 1);
+    critic_end = total = off;
+  }
+};
+
+// ====================================================================== profiler
+struct ProfRec {
+  std::string name;
+  hipEvent_t e0, e1;
+  double flops, bytes;
+};
+struct ProfAgg {
+  double ms = 0, flops = 0, bytes = 0;
+  int64_t launches = 0;
+};
+
+// ====================================================================== replay
+struct ddpg_replay {
+  int device = 0, S = 0, A = 0;
+  int64_t cap = 0, count = 0, total = 0;
+  float *rs = nullptr, *ra = nullptr, *rr = nullptr, *rt = nullptr, *rs2 = nullptr;
+  Sampler sampler;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // host staging for single-row adds
+  std::vector<float> st_s, st_a, st_r, st_t, st_s2;
+  int64_t st_first = 0;  // insertion index of first staged row
+  int st_n = 0;
+  std::vector<int64_t> tmp_idx;
+  std::vector<int> tmp_slot;
+  int* d_slots = nullptr;
+  int d_slots_cap = 0;
+  float* d_tmp = nullptr;
+  size_t d_tmp_cap = 0;
+  explicit ddpg_replay(int64_t seed) : sampler(seed) {}
+};
+
+static void replay_flush(ddpg_replay* rb);
+
+// ====================================================================== context
+struct ddpg_ctx {
+  ddpg_cfg cfg{};
+  Layout L;
+  int S, A, H1, H2, Bmax;
+  int ldS, ldA, ldH1, ldH2, ldC;
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  std::string err;
+
+  // parameters (fp32 master) -- one allocation: theta|target|m|v|grad
+  float* dparams = nullptr;
+  float *theta = nullptr, *target = nullptr, *adam_m = nullptr, *adam_v = nullptr,
+        *grad = nullptr;
+  float* dpw = nullptr;          // [actor b1p, b2p, critic b1p, b2p]
+  unsigned* dcounter = nullptr;  // [2]
+  float* dstats = nullptr;       // [q_max, loss]
+  double* dacc = nullptr;        // [qmax_sum, loss_sum, steps]
+  double *dmean = nullptr, *dscale = nullptr;
+  bool has_scaler = false;
+
+  // activations / workspaces
+  float* dact = nullptr;
+  float *s, *s2, *a, *r, *t, *y, *q, *dq;
+  float *th1, *tcat, *ta2, *cat, *h, *dhp, *dcat;
+  float *h1, *h2, *o, *mu, *cat2, *dhp2, *da, *dz3, *dz2, *dz1, *dain;
+  float *ppart, *qpart, *colpart, *headpart;  // partial-sum scratch
+  float *slab_W1, *slab_W2, *slab_W3, *slab_Ws, *slab_Wa, *slab_Wh;
+  int split_cap_W1, split_cap_W2, split_cap_W3, split_cap_Ws, split_cap_Wa, split_cap_Wh;
+  int* d_slots = nullptr;
+  int* h_slots = nullptr;  // pinned, kSlotRing x Bmax
+  hipEvent_t slot_ev[4];
+  int slot_i = 0;
+  std::vector<int64_t> idx_tmp;
+
+  // comm
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+
+  // profiling
+  bool prof = false;
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, ProfAgg> prof_agg;
+};
+
+static constexpr int kSlotRing = 4;
+static constexpr int kHeadRows = 64;
+
+// ---------------------------------------------------------------- profiling helpers
+static hipEvent_t ev_get(ddpg_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  HIP_TRY(hipEventCreate(&e));
+  return e;
+}
+
+struct ProfScope {
+  ddpg_ctx* c;
+  size_t idx = (size_t)-1;
+  ProfScope(ddpg_ctx* ctx, const char* name, double flops, double bytes) : c(ctx) {
+    if (!c->prof) return;
+    ProfRec rec{name, ev_get(c), ev_get(c), flops, bytes};
+    HIP_TRY(hipEventRecord(rec.e0, c->stream));
+    c->prof_recs.push_back(rec);
+    idx = c->prof_recs.size() - 1;
+  }
+  ~ProfScope() {
+    if (idx != (size_t)-1) (void)hipEventRecord(c->prof_recs[idx].e1, c->stream);
+  }
+};
+
+static void prof_collect(ddpg_ctx* c) {
+  if (c->prof_recs.empty()) return;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto& r : c->prof_recs) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, r.e0, r.e1));
+    ProfAgg& a = c->prof_agg[r.name];
+    a.ms += ms;
+    a.flops += r.flops;
+    a.bytes += r.bytes;
+    a.launches += 1;
+    c->ev_pool.push_back(r.e0);
+    c->ev_pool.push_back(r.e1);
+  }
+  c->prof_recs.clear();
+}
+
+// ---------------------------------------------------------------- GEMM launch
+static GemmEpi epi_none() {
+  GemmEpi e;
+  memset(&e, 0, sizeof e);
+  return e;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int AL, int BL>
+static void gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda, const float* B,
+                        int ldb, int M, int N, int K, const GemmEpi& e, int splits = 1) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs g;
+  g.A = A;
+  g.B = B;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = lda;
+  g.ldb = ldb;
+  splits = std::max(1, splits);
+  int kps = rup(std::max(1, ceil_div(K, splits)), GBK);
+  splits = std::max(1, ceil_div(K, kps));
+  g.kps = kps;
+  g.e = e;
+  const int contA = (AL == L_RK) ? K : M;
+  const int contB = (BL == L_RK) ? K : N;
+  const bool vec = (contA % 4 == 0) && (contB % 4 == 0) && (lda % 4 == 0) && (ldb % 4 == 0) &&
+                   aligned16(A) && aligned16(B);
+  dim3 grid(ceil_div(N, GBN), ceil_div(M, GBM), splits);
+  ProfScope ps(c, name, 2.0 * M * N * (double)K, 0.0);
+  if (vec)
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, 4>), grid, dim3(GNT), 0, c->stream, g);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, 1>), grid, dim3(GNT), 0, c->stream, g);
+  HIP_TRY(hipGetLastError());
+}
+
+// weight-grad split: aim for ~2 blocks per CU, >= 256 k per split
+static int wgrad_splits(int M, int N, int K) {
+  const int tiles = ceil_div(M, GBM) * ceil_div(N, GBN);
+  int s = std::max(1, 512 / tiles);
+  s = std::min(s, std::max(1, K / 256));
+  return std::min(s, 64);
+}
+
+// ====================================================================== building blocks
+static const float* P(ddpg_ctx* c, const float* base, const Tensor& t) { return base + t.off; }
+
+// Actor forward (networks.py:51-63) on [B][ldS] states.
+// h1 is always materialised (input of layer 2); h2 only when store_h2.
+static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, float* h1,
+                      float* h2, float* o, float* mu) {
+  const Layout& L = c->L;
+  GemmEpi e = epi_none();
+  e.out = h1;
+  e.ldo = c->ldH1;
+  e.bias = P(c, base, L.a[AB1]);
+  e.act = 1;
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.a[AW1]), c->H1, B, c->H1, c->S,
+                          e);
+  e = epi_none();
+  e.out = h2;
+  e.ldo = c->ldH2;
+  e.bias = P(c, base, L.a[AB2]);
+  e.act = 1;
+  e.proj = P(c, base, L.a[AW3]);
+  e.proj_n = c->A;
+  e.proj_sn = c->A;
+  e.proj_sa = 1;
+  e.proj_out = c->ppart;
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd_head", h1, c->ldH1, P(c, base, L.a[AW2]), c->H2, B,
+                          c->H2, c->H1, e);
+  const int NT = ceil_div(c->H2, GBN);
+  {
+    ProfScope ps(c, "actor_out", 0, 0);
+    hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
+                       c->ppart, NT, B, c->A, c->cfg.action_scale, o, mu, c->ldA);
+    HIP_TRY(hipGetLastError());
+  }
+}
+
+// Critic first layer + hidden layer (networks.py:147-161).  mode:
+//   0: store h (train), proj(Wo) -> qpart
+//   1: proj(Wo) -> qpart only (predict / target)
+//   2: dh_pre = Wo[j] * elu'(h) -> dhp_out (action-gradient path, grad_ys = 1)
+static void critic_fwd(ddpg_ctx* c, const float* base, const float* s, const float* a, int B,
+                       float* cat, float* h_out, int mode, float* dhp_out) {
+  const Layout& L = c->L;
+  GemmEpi e = epi_none();
+  e.out = cat;
+  e.ldo = c->ldC;
+  e.bias = P(c, base, L.c[CBS]);
+  e.act = 1;
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.c[CWS]), c->H1, B, c->H1, c->S,
+                          e);
+  e.out = cat + c->H1;
+  e.bias = P(c, base, L.c[CBA]);
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", a, c->ldA, P(c, base, L.c[CWA]), c->H1, B, c->H1, c->A,
+                          e);
+  e = epi_none();
+  e.bias = P(c, base, L.c[CBH]);
+  e.act = 1;
+  if (mode == 2) {
+    e.post = 2;
+    e.pw = P(c, base, L.c[CWO]);
+    e.out = dhp_out;
+    e.ldo = c->ldH2;
+  } else {
+    e.out = (mode == 0) ? h_out : nullptr;
+    e.ldo = c->ldH2;
+    e.proj = P(c, base, L.c[CWO]);
+    e.proj_n = 1;
+    e.proj_sn = 1;
+    e.proj_sa = 0;
+    e.proj_out = c->qpart;
+  }
+  gemm_launch<L_RK, L_KR>(c, mode == 2 ? "gemm_fwd" : "gemm_fwd_head", cat, c->ldC,
+                          P(c, base, L.c[CWH]), c->H2, B, c->H2, 2 * c->H1, e);
+}
+
+// dQ/da of the (already updated) online critic at (s, a): networks.py:143.
+// Writes da (optional, [B][ldA]) and dz3 = actor grad_ys chain (optional).
+static void critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int B, float* da,
+                               float* dz3, const float* o) {
+  const Layout& L = c->L;
+  critic_fwd(c, c->theta, s, a, B, c->cat2, nullptr, 2, c->dhp2);
+  GemmEpi e = epi_none();
+  e.post = 1;
+  e.aux = c->cat2 + c->H1;
+  e.ldaux = c->ldC;
+  e.proj = P(c, c->theta, L.c[CWA]);
+  e.proj_n = c->A;
+  e.proj_sn = 1;
+  e.proj_sa = c->H1;
+  e.proj_out = c->ppart;
+  // B operand = Wh[H1:2H1, :]^T  (NK: element (k=j, n=i) at Wh[(H1+i)*H2 + j])
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp2, c->ldH2,
+                          P(c, c->theta, L.c[CWH]) + (size_t)c->H1 * c->H2, c->H2, B, c->H1, c->H2,
+                          e);
+  ProfScope ps(c, "action_grad", 0, 0);
+  hipLaunchKernelGGL(action_grad_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
+                     c->ppart, ceil_div(c->H1, GBN), B, c->A, B, o, c->ldA,
+                     c->cfg.action_scale, da, dz3);
+  HIP_TRY(hipGetLastError());
+}
+
+static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
+  long long tot = 0;
+  for (int i = 0; i < tab.nseg; ++i) {
+    tab.start[i] = tot;
+    tot += (long long)tab.seg[i].rows * tab.seg[i].cols;
+  }
+  tab.start[tab.nseg] = tot;
+  double bytes = 0;
+  for (int i = 0; i < tab.nseg; ++i)
+    bytes += (double)tab.seg[i].rows * tab.seg[i].cols * 4.0 * (tab.seg[i].nslab + 1);
+  ProfScope ps(c, name, 0, bytes);
+  int blocks = (int)std::min<long long>(2048, (tot + 255) / 256);
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(std::max(1, blocks)), dim3(256), 0, c->stream, tab);
+  HIP_TRY(hipGetLastError());
+}
+
+static void add_seg(ReduceTable& t, const float* src, float* dst, long long stride, int nslab,
+                    int rows, int cols, int src_ld) {
+  ReduceSeg& s = t.seg[t.nseg++];
+  s.src = src;
+  s.dst = dst;
+  s.slab_stride = stride;
+  s.nslab = nslab;
+  s.rows = rows;
+  s.cols = cols;
+  s.src_ld = src_ld;
+}
+
+static void allreduce(ddpg_ctx* c, float* buf, size_t n) {
+  if (c->world <= 1 || !c->comm) return;
+  ProfScope ps(c, "rccl_allreduce", 0, (double)n * 4.0);
+  ncclResult_t r = ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, c->comm, c->stream);
+  if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
+}
+
+static void adam_launch(ddpg_ctx* c, int net) {
+  const size_t b = net == 0 ? c->L.actor_begin : c->L.critic_begin;
+  const size_t e = net == 0 ? c->L.actor_end : c->L.critic_end;
+  const long long n = (long long)(e - b);
+  const float lr = net == 0 ? c->cfg.actor_lr : c->cfg.critic_lr;
+  int blocks = (int)std::min<long long>(2048, std::max<long long>(1, (n / 4 + 255) / 256));
+  ProfScope ps(c, "adam", 0, 28.0 * n);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
+                     c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net,
+                     c->dcounter + net, lr, c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon);
+  HIP_TRY(hipGetLastError());
+}
+
+// Critic update on rows already in c->s / c->a with targets in c->y.
+// networks.py:130-137,170-175 (+ RCCL sum over ranks for world > 1).
+static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
+  const Layout& L = c->L;
+  critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
+  {
+    ProfScope ps(c, "critic_loss", 0, 0);
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->stream, c->qpart,
+                       ceil_div(c->H2, GBN), B, P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q,
+                       c->dq, c->dstats, c->dacc);
+    HIP_TRY(hipGetLastError());
+  }
+  const int nchunk = ceil_div(B, kHeadRows);
+  float* part_dWo = c->headpart;
+  float* part_dbh = c->headpart + (size_t)nchunk * c->H2;
+  float* part_dbo = part_dbh + (size_t)nchunk * c->H2;
+  {
+    ProfScope ps(c, "critic_head_bwd", 0, (double)B * c->H2 * 8.0);
+    hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->H2, 256), nchunk), dim3(256), 0,
+                       c->stream, c->h, c->ldH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->H2,
+                       kHeadRows, c->dhp, c->ldH2, part_dWo, part_dbh, part_dbo);
+    HIP_TRY(hipGetLastError());
+  }
+  // dWh = cat^T . dh_pre   (split-K slabs)
+  const int sWh = std::min(c->split_cap_Wh, wgrad_splits(2 * c->H1, c->H2, B));
+  GemmEpi e = epi_none();
+  e.out = c->slab_Wh;
+  e.ldo = c->H2;
+  e.out_split_stride = (long long)2 * c->H1 * c->H2;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->cat, c->ldC, c->dhp, c->ldH2, 2 * c->H1, c->H2, B,
+                          e, sWh);
+  // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
+  const int mt = ceil_div(B, GBM);
+  e = epi_none();
+  e.post = 1;
+  e.aux = c->cat;
+  e.ldaux = c->ldC;
+  e.out = c->dcat;
+  e.ldo = c->ldC;
+  e.colsum = c->colpart;
+  e.ld_colsum = 2 * c->H1;
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp, c->ldH2, P(c, c->theta, L.c[CWH]), c->H2, B,
+                          2 * c->H1, c->H2, e);
+  // dWs = s^T . dcs ; dWa = a^T . dca
+  const int sWs = std::min(c->split_cap_Ws, wgrad_splits(c->S, c->H1, B));
+  e = epi_none();
+  e.out = c->slab_Ws;
+  e.ldo = c->H1;
+  e.out_split_stride = (long long)c->S * c->H1;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->H1, B, e, sWs);
+  const int sWa = std::min(c->split_cap_Wa, wgrad_splits(c->A, c->H1, B));
+  e.out = c->slab_Wa;
+  e.out_split_stride = (long long)c->A * c->H1;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->a, c->ldA, c->dcat + c->H1, c->ldC, c->A, c->H1, B,
+                          e, sWa);
+  // gather every critic gradient into the flat grad buffer
+  float* G = c->grad;
+  ReduceTable tab;
+  tab.nseg = 0;
+  const long long kps_unused = 0;
+  (void)kps_unused;
+  auto gsplits = [&](int s, int K) {  // effective split count used by gemm_launch
+    int kps = rup(std::max(1, ceil_div(K, s)), GBK);
+    return std::max(1, ceil_div(K, kps));
+  };
+  add_seg(tab, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->H1, gsplits(sWs, B), c->S,
+          c->H1, c->H1);
+  add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->H1, mt, 1, c->H1, 0);
+  add_seg(tab, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->H1, gsplits(sWa, B), c->A,
+          c->H1, c->H1);
+  add_seg(tab, c->colpart + c->H1, G + L.c[CBA].off, 2 * c->H1, mt, 1, c->H1, 0);
+  add_seg(tab, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->H1 * c->H2, gsplits(sWh, B),
+          2 * c->H1, c->H2, c->H2);
+  add_seg(tab, part_dbh, G + L.c[CBH].off, c->H2, nchunk, 1, c->H2, 0);
+  add_seg(tab, part_dWo, G + L.c[CWO].off, c->H2, nchunk, 1, c->H2, 0);
+  add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1, 1, 0);
+  reduce_launch(c, "grad_reduce", tab);
+  allreduce(c, G + L.critic_begin, L.critic_end - L.critic_begin);
+  adam_launch(c, 1);
+}
+
+// Actor update given dz3 (= TanhGrad chain of -dQ/da) and the forward
+// activations h1, h2 of c->s.  networks.py:39-47,71-75.
+static void actor_train_dev(ddpg_ctx* c, int B) {
+  const Layout& L = c->L;
+  float* G = c->grad;
+  const int mt = ceil_div(B, GBM);
+  // dW3 = h2^T . dz3
+  const int sW3 = std::min(c->split_cap_W3, wgrad_splits(c->H2, c->A, B));
+  GemmEpi e = epi_none();
+  e.out = c->slab_W3;
+  e.ldo = c->A;
+  e.out_split_stride = (long long)c->H2 * c->A;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h2, c->ldH2, c->dz3, c->ldA, c->H2, c->A, B, e, sW3);
+  // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
+  e = epi_none();
+  e.post = 1;
+  e.aux = c->h2;
+  e.ldaux = c->ldH2;
+  e.out = c->dz2;
+  e.ldo = c->ldH2;
+  e.colsum = c->colpart;
+  e.ld_colsum = c->H2;
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A, B, c->H2,
+                          c->A, e);
+  // dW2 = h1^T . dz2
+  const int sW2 = std::min(c->split_cap_W2, wgrad_splits(c->H1, c->H2, B));
+  e = epi_none();
+  e.out = c->slab_W2;
+  e.ldo = c->H2;
+  e.out_split_stride = (long long)c->H1 * c->H2;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h1, c->ldH1, c->dz2, c->ldH2, c->H1, c->H2, B, e,
+                          sW2);
+  // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
+  float* colpart1 = c->colpart + (size_t)mt * c->H2;
+  e = epi_none();
+  e.post = 1;
+  e.aux = c->h1;
+  e.ldaux = c->ldH1;
+  e.out = c->dz1;
+  e.ldo = c->ldH1;
+  e.colsum = colpart1;
+  e.ld_colsum = c->H1;
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz2, c->ldH2, P(c, c->theta, L.a[AW2]), c->H2, B,
+                          c->H1, c->H2, e);
+  // dW1 = s^T . dz1
+  const int sW1 = std::min(c->split_cap_W1, wgrad_splits(c->S, c->H1, B));
+  e = epi_none();
+  e.out = c->slab_W1;
+  e.ldo = c->H1;
+  e.out_split_stride = (long long)c->S * c->H1;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dz1, c->ldH1, c->S, c->H1, B, e, sW1);
+
+  auto gsplits = [&](int s, int K) {
+    int kps = rup(std::max(1, ceil_div(K, s)), GBK);
+    return std::max(1, ceil_div(K, kps));
+  };
+  ReduceTable tab;
+  tab.nseg = 0;
+  add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->H1, gsplits(sW1, B), c->S, c->H1,
+          c->H1);
+  add_seg(tab, colpart1, G + L.a[AB1].off, c->H1, mt, 1, c->H1, 0);
+  add_seg(tab, c->slab_W2, G + L.a[AW2].off, (long long)c->H1 * c->H2, gsplits(sW2, B), c->H1,
+          c->H2, c->H2);
+  add_seg(tab, c->colpart, G + L.a[AB2].off, c->H2, mt, 1, c->H2, 0);
+  add_seg(tab, c->slab_W3, G + L.a[AW3].off, (long long)c->H2 * c->A, gsplits(sW3, B), c->H2,
+          c->A, c->A);
+  reduce_launch(c, "grad_reduce", tab);
+  allreduce(c, G + L.actor_begin, L.actor_end - L.actor_begin);
+  adam_launch(c, 0);
+}
+
+static void soft_update_dev(ddpg_ctx* c, int mask) {
+  const float tau = c->cfg.tau;
+  const float omt = (float)(1.0 - (double)tau);
+  auto run = [&](size_t b, size_t e) {
+    const long long n = (long long)(e - b);
+    int blocks = (int)std::min<long long>(2048, std::max<long long>(1, (n / 4 + 255) / 256));
+    ProfScope ps(c, "soft_update", 0, 12.0 * n);
+    hipLaunchKernelGGL(soft_update_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
+                       c->target + b, n, tau, omt);
+    HIP_TRY(hipGetLastError());
+  };
+  if ((mask & DDPG_SOFT_ACTOR) && (mask & DDPG_SOFT_CRITIC))
+    run(c->L.actor_begin, c->L.critic_end);
+  else if (mask & DDPG_SOFT_ACTOR)
+    run(c->L.actor_begin, c->L.actor_end);
+  else if (mask & DDPG_SOFT_CRITIC)
+    run(c->L.critic_begin, c->L.critic_end);
+}
+
+// One full learner step (ddpg.py:86-113) on rows already gathered into
+// c->s, c->a, c->r, c->t, c->s2 (B local rows, inv_b = 1/B_global).
+static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
+  const Layout& L = c->L;
+  // target_q = critic.predict_target(s2, actor.predict_target(s2))  ddpg.py:90
+  actor_fwd(c, c->target, c->s2, B, c->th1, nullptr, nullptr, c->ta2);
+  critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr);
+  {
+    ProfScope ps(c, "td_target", 0, 0);
+    hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
+                       ceil_div(c->H2, GBN), B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t,
+                       c->cfg.gamma, c->y);
+    HIP_TRY(hipGetLastError());
+  }
+  // critic.train(s, a, y)  ddpg.py:100
+  critic_train_dev(c, B, inv_b);
+  // a_outs = actor.predict(s); grads = critic.action_gradients(s, a_outs)  ddpg.py:106-107
+  actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu);
+  critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);
+  // actor.train(s, grads[0])  ddpg.py:109  (forward above reused: same params)
+  actor_train_dev(c, B);
+  // actor/critic.update_target_network()  ddpg.py:112-113
+  soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC);
+}
+
+// ====================================================================== helpers
+static void upload_rows(ddpg_ctx* c, float* dst, int ld, const float* src, int B, int cols) {
+  if (B <= 0 || cols <= 0) return;
+  HIP_TRY(hipMemcpy2DAsync(dst, (size_t)ld * 4, src, (size_t)cols * 4, (size_t)cols * 4, B,
+                           hipMemcpyHostToDevice, c->stream));
+}
+static void download_rows(ddpg_ctx* c, float* dst, const float* src, int ld, int B, int cols) {
+  if (B <= 0 || cols <= 0) return;
+  HIP_TRY(hipMemcpy2DAsync(dst, (size_t)cols * 4, src, (size_t)ld * 4, (size_t)cols * 4, B,
+                           hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+}
+
+static void check_b(ddpg_ctx* c, int B) {
+  if (B <= 0 || B > c->Bmax) throw einval("batch %d outside [1, %d]", B, c->Bmax);
+}
+
+static void apply_scaler(ddpg_ctx* c, float* x, int B) {
+  if (!c->has_scaler) return;
+  hipLaunchKernelGGL(scale_rows_kernel, dim3(ceil_div(B * c->S, 256)), dim3(256), 0, c->stream, x,
+                     B, c->S, c->ldS, c->dmean, c->dscale);
+  HIP_TRY(hipGetLastError());
+}
+
+template <class F>
+static int guard(ddpg_ctx* c, F&& f) {
+  try {
+    f();
+    return DDPG_OK;
+  } catch (const DdpgError& e) {
+    if (c) c->err = e.msg;
+    g_err = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    if (c) c->err = e.what();
+    g_err = e.what();
+    return DDPG_ENOMEM;
+  }
+}
+
+static void ctx_free(ddpg_ctx* c) {
+  if (!c) return;
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (auto& r : c->prof_recs) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < kSlotRing; ++i)
+    if (c->slot_ev[i]) (void)hipEventDestroy(c->slot_ev[i]);
+  if (c->h_slots) (void)hipHostFree(c->h_slots);
+  for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
+                  (void*)c->dmean, (void*)c->dscale, (void*)c->dacc})
+    if (p) (void)hipFree(p);
+  if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+template <class F>
+static int rguard(ddpg_replay* rb, F&& f) {
+  try {
+    f();
+    return DDPG_OK;
+  } catch (const DdpgError& e) {
+    if (rb) rb->err = e.msg;
+    g_err = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    if (rb) rb->err = e.what();
+    g_err = e.what();
+    return DDPG_ENOMEM;
+  }
+}
+
+// ====================================================================== C ABI
+extern "C" {
+
+int ddpg_abi_version(void) { return DDPG_ABI_VERSION; }
+const char* ddpg_global_error(void) { return g_err.c_str(); }
+const char* ddpg_last_error(ddpg_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
+  if (!cfg || !out) {
+    g_err = "null argument";
+    return DDPG_EINVAL;
+  }
+  ddpg_ctx* c = new ddpg_ctx();
+  memset(c->slot_ev, 0, sizeof c->slot_ev);
+  int rc = guard(c, [&] {
+    const ddpg_cfg& k = *cfg;
+    if (k.state_dim <= 0 || k.action_dim <= 0 || k.h1 <= 0 || k.h2 <= 0 || k.batch_max <= 0)
+      throw einval("dims must be positive (S=%d A=%d H1=%d H2=%d Bmax=%d)", k.state_dim,
+                   k.action_dim, k.h1, k.h2, k.batch_max);
+    if (k.action_dim > PROJ_MAX) throw einval("action_dim %d > %d", k.action_dim, PROJ_MAX);
+    if (k.dtype != DDPG_FP32) throw einval("dtype %d not supported by this build", k.dtype);
+    c->cfg = k;
+    c->S = k.state_dim;
+    c->A = k.action_dim;
+    c->H1 = k.h1;
+    c->H2 = k.h2;
+    c->Bmax = k.batch_max;
+    c->world = std::max(1, k.world);
+    c->rank = k.rank;
+    c->ldS = rup(c->S, 4);
+    c->ldA = rup(c->A, 4);
+    c->ldH1 = rup(c->H1, 4);
+    c->ldH2 = rup(c->H2, 4);
+    c->ldC = rup(2 * c->H1, 4);
+    c->L.build(c->S, c->A, c->H1, c->H2);
+    HIP_TRY(hipSetDevice(k.device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const size_t PT = c->L.total;
+    HIP_TRY(hipMalloc(&c->dparams, 5 * PT * sizeof(float)));
+    HIP_TRY(hipMemset(c->dparams, 0, 5 * PT * sizeof(float)));
+    c->theta = c->dparams;
+    c->target = c->dparams + PT;
+    c->adam_m = c->dparams + 2 * PT;
+    c->adam_v = c->dparams + 3 * PT;
+    c->grad = c->dparams + 4 * PT;
+    HIP_TRY(hipMalloc(&c->dpw, 64));
+    {
+      float pw[8] = {k.beta1, k.beta2, k.beta1, k.beta2, 0, 0, 0, 0};
+      HIP_TRY(hipMemcpy(c->dpw, pw, sizeof pw, hipMemcpyHostToDevice));
+    }
+    c->dcounter = reinterpret_cast<unsigned*>(c->dpw + 4);
+    c->dstats = c->dpw + 6;
+    HIP_TRY(hipMalloc(&c->dacc, 4 * sizeof(double)));
+    HIP_TRY(hipMemset(c->dacc, 0, 4 * sizeof(double)));
+
+    // activation workspace
+    const size_t B = (size_t)c->Bmax;
+    const int NT2 = ceil_div(c->H2, GBN), NT1 = ceil_div(c->H1, GBN);
+    const int mt = ceil_div(c->Bmax, GBM);
+    const int nchunk = ceil_div(c->Bmax, kHeadRows);
+    c->split_cap_W1 = wgrad_splits(c->S, c->H1, c->Bmax);
+    c->split_cap_W2 = wgrad_splits(c->H1, c->H2, c->Bmax);
+    c->split_cap_W3 = wgrad_splits(c->H2, c->A, c->Bmax);
+    c->split_cap_Ws = wgrad_splits(c->S, c->H1, c->Bmax);
+    c->split_cap_Wa = wgrad_splits(c->A, c->H1, c->Bmax);
+    c->split_cap_Wh = wgrad_splits(2 * c->H1, c->H2, c->Bmax);
+    struct Req {
+      float** p;
+      size_t n;
+    };
+    std::vector<Req> req = {
+        {&c->s, B * c->ldS},   {&c->s2, B * c->ldS},   {&c->a, B * c->ldA},
+        {&c->r, B},            {&c->t, B},             {&c->y, B},
+        {&c->q, B},            {&c->dq, B},            {&c->th1, B * c->ldH1},
+        {&c->tcat, B * c->ldC}, {&c->ta2, B * c->ldA}, {&c->cat, B * c->ldC},
+        {&c->h, B * c->ldH2},  {&c->dhp, B * c->ldH2}, {&c->dcat, B * c->ldC},
+        {&c->h1, B * c->ldH1}, {&c->h2, B * c->ldH2},  {&c->o, B * c->ldA},
+        {&c->mu, B * c->ldA},  {&c->cat2, B * c->ldC}, {&c->dhp2, B * c->ldH2},
+        {&c->da, B * c->ldA},  {&c->dz3, B * c->ldA},  {&c->dz2, B * c->ldH2},
+        {&c->dz1, B * c->ldH1}, {&c->dain, B * c->A},
+        {&c->ppart, (size_t)std::max(NT1, NT2) * B * PROJ_MAX},
+        {&c->qpart, (size_t)NT2 * B},
+        {&c->colpart, (size_t)mt * (c->H2 + std::max(2 * c->H1, c->H1))},
+        {&c->headpart, (size_t)nchunk * (2 * c->H2 + 1)},
+        {&c->slab_W1, (size_t)c->split_cap_W1 * c->S * c->H1},
+        {&c->slab_W2, (size_t)c->split_cap_W2 * c->H1 * c->H2},
+        {&c->slab_W3, (size_t)c->split_cap_W3 * c->H2 * c->A},
+        {&c->slab_Ws, (size_t)c->split_cap_Ws * c->S * c->H1},
+        {&c->slab_Wa, (size_t)c->split_cap_Wa * c->A * c->H1},
+        {&c->slab_Wh, (size_t)c->split_cap_Wh * 2 * c->H1 * c->H2},
+    };
+    size_t tot = 0;
+    for (auto& r : req) tot += (r.n + 63) / 64 * 64;
+    HIP_TRY(hipMalloc(&c->dact, tot * sizeof(float)));
+    HIP_TRY(hipMemset(c->dact, 0, tot * sizeof(float)));
+    size_t off = 0;
+    for (auto& r : req) {
+      *r.p = c->dact + off;
+      off += (r.n + 63) / 64 * 64;
+    }
+    HIP_TRY(hipMalloc(&c->d_slots, B * sizeof(int)));
+    HIP_TRY(hipHostMalloc(&c->h_slots, kSlotRing * B * sizeof(int)));
+    for (int i = 0; i < kSlotRing; ++i) HIP_TRY(hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming));
+    c->idx_tmp.resize(B * c->world);
+    HIP_TRY(hipDeviceSynchronize());
+  });
+  if (rc != DDPG_OK) {
+    ctx_free(c);
+    *out = nullptr;
+    return rc;
+  }
+  *out = c;
+  return DDPG_OK;
+}
+
+void ddpg_destroy(ddpg_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  ctx_free(c);
+}
+
+int ddpg_sync(ddpg_ctx* c) {
+  return guard(c, [&] { HIP_TRY(hipStreamSynchronize(c->stream)); });
+}
+
+int ddpg_set_stream(ddpg_ctx* c, void* s) {
+  return guard(c, [&] {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->own_stream) HIP_TRY(hipStreamDestroy(c->stream));
+    if (s) {
+      c->stream = (hipStream_t)s;
+      c->own_stream = false;
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      c->own_stream = true;
+    }
+  });
+}
+
+// ---------------------------------------------------------------- parameters
+static void which_tensors(ddpg_ctx* c, int which, const Tensor** ts, int* nt, float** base) {
+  const bool actor = which == DDPG_ACTOR || which == DDPG_ACTOR_TARGET ||
+                     which == DDPG_ACTOR_ADAM_M || which == DDPG_ACTOR_ADAM_V;
+  *ts = actor ? c->L.a : c->L.c;
+  *nt = actor ? NA : NC;
+  switch (which) {
+    case DDPG_ACTOR:
+    case DDPG_CRITIC: *base = c->theta; break;
+    case DDPG_ACTOR_TARGET:
+    case DDPG_CRITIC_TARGET: *base = c->target; break;
+    case DDPG_ACTOR_ADAM_M:
+    case DDPG_CRITIC_ADAM_M: *base = c->adam_m; break;
+    case DDPG_ACTOR_ADAM_V:
+    case DDPG_CRITIC_ADAM_V: *base = c->adam_v; break;
+    default: throw einval("bad parameter set %d", which);
+  }
+}
+
+int ddpg_param_count(ddpg_ctx* c, int which, size_t* n) {
+  return guard(c, [&] {
+    const Tensor* ts;
+    int nt;
+    float* base;
+    which_tensors(c, which, &ts, &nt, &base);
+    size_t tot = 0;
+    for (int i = 0; i < nt; ++i) tot += ts[i].count();
+    *n = tot;
+  });
+}
+
+int ddpg_set_params(ddpg_ctx* c, int which, const float* host, size_t n) {
+  return guard(c, [&] {
+    const Tensor* ts;
+    int nt;
+    float* base;
+    which_tensors(c, which, &ts, &nt, &base);
+    size_t tot = 0;
+    for (int i = 0; i < nt; ++i) tot += ts[i].count();
+    if (n != tot) throw einval("param set %d expects %zu floats, got %zu", which, tot, n);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    size_t o = 0;
+    for (int i = 0; i < nt; ++i) {
+      HIP_TRY(hipMemcpy(base + ts[i].off, host + o, ts[i].count() * 4, hipMemcpyHostToDevice));
+      o += ts[i].count();
+    }
+  });
+}
+
+int ddpg_get_params(ddpg_ctx* c, int which, float* host, size_t n) {
+  return guard(c, [&] {
+    const Tensor* ts;
+    int nt;
+    float* base;
+    which_tensors(c, which, &ts, &nt, &base);
+    size_t tot = 0;
+    for (int i = 0; i < nt; ++i) tot += ts[i].count();
+    if (n != tot) throw einval("param set %d has %zu floats, buffer %zu", which, tot, n);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    size_t o = 0;
+    for (int i = 0; i < nt; ++i) {
+      HIP_TRY(hipMemcpy(host + o, base + ts[i].off, ts[i].count() * 4, hipMemcpyDeviceToHost));
+      o += ts[i].count();
+    }
+  });
+}
+
+int ddpg_set_adam_powers(ddpg_ctx* c, int net, float b1p, float b2p) {
+  return guard(c, [&] {
+    if (net != 0 && net != 1) throw einval("net must be 0 (actor) or 1 (critic)");
+    float pw[2] = {b1p, b2p};
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->dpw + 2 * net, pw, sizeof pw, hipMemcpyHostToDevice));
+  });
+}
+
+int ddpg_get_adam_powers(ddpg_ctx* c, int net, float* b1p, float* b2p) {
+  return guard(c, [&] {
+    if (net != 0 && net != 1) throw einval("net must be 0 (actor) or 1 (critic)");
+    float pw[2];
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(pw, c->dpw + 2 * net, sizeof pw, hipMemcpyDeviceToHost));
+    *b1p = pw[0];
+    *b2p = pw[1];
+  });
+}
+
+int ddpg_set_scaler(ddpg_ctx* c, const double* mean, const double* scale, int S) {
+  return guard(c, [&] {
+    if (!mean || !scale) {
+      c->has_scaler = false;
+      return;
+    }
+    if (S != c->S) throw einval("scaler has %d features, state_dim is %d", S, c->S);
+    if (!c->dmean) {
+      HIP_TRY(hipMalloc(&c->dmean, S * sizeof(double)));
+      HIP_TRY(hipMalloc(&c->dscale, S * sizeof(double)));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->dmean, mean, S * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->dscale, scale, S * sizeof(double), hipMemcpyHostToDevice));
+    c->has_scaler = true;
+  });
+}
+
+// ---------------------------------------------------------------- 1:1 methods
+int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_out) {
+  return guard(c, [&] {
+    check_b(c, B);
+    upload_rows(c, c->s, c->ldS, s, B, c->S);
+    apply_scaler(c, c->s, B);
+    actor_fwd(c, target ? c->target : c->theta, c->s, B, c->h1, nullptr, nullptr, c->mu);
+    download_rows(c, a_out, c->mu, c->ldA, B, c->A);
+  });
+}
+
+int ddpg_critic_forward(ddpg_ctx* c, int target, const float* s, const float* a, int B,
+                        float* q_out) {
+  return guard(c, [&] {
+    check_b(c, B);
+    upload_rows(c, c->s, c->ldS, s, B, c->S);
+    apply_scaler(c, c->s, B);
+    upload_rows(c, c->a, c->ldA, a, B, c->A);
+    const float* base = target ? c->target : c->theta;
+    critic_fwd(c, base, c->s, c->a, B, c->cat, nullptr, 1, nullptr);
+    hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
+                       ceil_div(c->H2, GBN), B, P(c, base, c->L.c[CBO]), c->q, 0, nullptr,
+                       nullptr, 0.f, nullptr);
+    HIP_TRY(hipGetLastError());
+    download_rows(c, q_out, c->q, 1, B, 1);
+  });
+}
+
+int ddpg_critic_train(ddpg_ctx* c, const float* s, const float* a, const float* y, int B,
+                      float* q_pre, float* loss) {
+  return guard(c, [&] {
+    check_b(c, B);
+    upload_rows(c, c->s, c->ldS, s, B, c->S);
+    apply_scaler(c, c->s, B);
+    upload_rows(c, c->a, c->ldA, a, B, c->A);
+    upload_rows(c, c->y, 1, y, B, 1);
+    critic_train_dev(c, B, 1.0f / (float)(B * c->world));
+    if (q_pre) download_rows(c, q_pre, c->q, 1, B, 1);
+    if (loss) {
+      float st[2];
+      HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      *loss = st[1];
+    }
+  });
+}
+
+int ddpg_critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int B, float* da) {
+  return guard(c, [&] {
+    check_b(c, B);
+    upload_rows(c, c->s, c->ldS, s, B, c->S);
+    apply_scaler(c, c->s, B);
+    upload_rows(c, c->a, c->ldA, a, B, c->A);
+    critic_action_grad(c, c->s, c->a, B, c->da, nullptr, nullptr);
+    download_rows(c, da, c->da, c->ldA, B, c->A);
+  });
+}
+
+int ddpg_actor_train(ddpg_ctx* c, const float* s, const float* a_gradient, int B) {
+  return guard(c, [&] {
+    check_b(c, B);
+    upload_rows(c, c->s, c->ldS, s, B, c->S);
+    apply_scaler(c, c->s, B);
+    // a_gradient as a single "partial" slab [1][B][A] for the dz3 finaliser
+    HIP_TRY(hipMemcpyAsync(c->dain, a_gradient, (size_t)B * c->A * 4, hipMemcpyHostToDevice,
+                           c->stream));
+    actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu);
+    hipLaunchKernelGGL(action_grad_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
+                       c->dain, 1, B, c->A, B, c->o, c->ldA, c->cfg.action_scale, nullptr,
+                       c->dz3);
+    HIP_TRY(hipGetLastError());
+    actor_train_dev(c, B);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  });
+}
+
+int ddpg_soft_update(ddpg_ctx* c, int mask) {
+  return guard(c, [&] {
+    soft_update_dev(c, mask);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  });
+}
+
+// ---------------------------------------------------------------- sampler
+struct ddpg_sampler {
+  Sampler s;
+  explicit ddpg_sampler(int64_t seed) : s(seed) {}
+};
+
+int ddpg_sampler_create(int64_t seed, ddpg_sampler** out) {
+  if (!out) return DDPG_EINVAL;
+  *out = new ddpg_sampler(seed);
+  return DDPG_OK;
+}
+void ddpg_sampler_destroy(ddpg_sampler* s) { delete s; }
+int ddpg_sampler_sample(ddpg_sampler* s, int64_t n, int k, int64_t* out) {
+  if (!s || !out || s->s.sample(n, k, out) != 0) {
+    g_err = "sample larger than population or is negative";
+    return DDPG_EINVAL;
+  }
+  return DDPG_OK;
+}
+int ddpg_sampler_getrandbits32(ddpg_sampler* s, uint32_t* out, int n) {
+  if (!s || !out || n < 0) return DDPG_EINVAL;
+  for (int i = 0; i < n; ++i) out[i] = s->s.rng.genrand_uint32();
+  return DDPG_OK;
+}
+
+// ---------------------------------------------------------------- replay
+static constexpr int kStageRows = 1024;
+
+int ddpg_replay_create(int device, int S, int A, int64_t cap, int64_t seed, ddpg_replay** out) {
+  if (!out) return DDPG_EINVAL;
+  ddpg_replay* rb = new ddpg_replay(seed);
+  int rc = rguard(rb, [&] {
+    if (S <= 0 || A <= 0 || cap <= 0) throw einval("bad replay dims S=%d A=%d cap=%lld", S, A,
+                                                   (long long)cap);
+    rb->device = device;
+    rb->S = S;
+    rb->A = A;
+    rb->cap = cap;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&rb->stream, hipStreamNonBlocking));
+    const size_t c = (size_t)cap;
+    HIP_TRY(hipMalloc(&rb->rs, c * S * 4));
+    HIP_TRY(hipMalloc(&rb->rs2, c * S * 4));
+    HIP_TRY(hipMalloc(&rb->ra, c * A * 4));
+    HIP_TRY(hipMalloc(&rb->rr, c * 4));
+    HIP_TRY(hipMalloc(&rb->rt, c * 4));
+    rb->st_s.resize((size_t)kStageRows * S);
+    rb->st_s2.resize((size_t)kStageRows * S);
+    rb->st_a.resize((size_t)kStageRows * A);
+    rb->st_r.resize(kStageRows);
+    rb->st_t.resize(kStageRows);
+  });
+  if (rc != DDPG_OK) {
+    ddpg_replay_destroy(rb);
+    *out = nullptr;
+    return rc;
+  }
+  *out = rb;
+  return DDPG_OK;
+}
+
+void ddpg_replay_destroy(ddpg_replay* rb) {
+  if (!rb) return;
+  (void)hipSetDevice(rb->device);
+  if (rb->stream) (void)hipStreamSynchronize(rb->stream);
+  for (void* p : {(void*)rb->rs, (void*)rb->rs2, (void*)rb->ra, (void*)rb->rr, (void*)rb->rt,
+                  (void*)rb->d_slots, (void*)rb->d_tmp})
+    if (p) (void)hipFree(p);
+  if (rb->stream) (void)hipStreamDestroy(rb->stream);
+  delete rb;
+}
+
+const char* ddpg_replay_last_error(ddpg_replay* rb) { return rb ? rb->err.c_str() : ""; }
+
+// copy n consecutive insertions starting at insertion index `first` into the ring
+static void ring_write(ddpg_replay* rb, int64_t first, int n, const float* s, const float* a,
+                       const float* r, const float* t, const float* s2) {
+  int done = 0;
+  while (done < n) {
+    const int64_t slot = (first + done) % rb->cap;
+    const int run = (int)std::min<int64_t>(n - done, rb->cap - slot);
+    const size_t S = rb->S, A = rb->A;
+    HIP_TRY(hipMemcpyAsync(rb->rs + slot * S, s + done * S, run * S * 4, hipMemcpyHostToDevice,
+                           rb->stream));
+    HIP_TRY(hipMemcpyAsync(rb->rs2 + slot * S, s2 + done * S, run * S * 4,
+                           hipMemcpyHostToDevice, rb->stream));
+    HIP_TRY(hipMemcpyAsync(rb->ra + slot * A, a + done * A, run * A * 4, hipMemcpyHostToDevice,
+                           rb->stream));
+    HIP_TRY(hipMemcpyAsync(rb->rr + slot, r + done, run * 4, hipMemcpyHostToDevice, rb->stream));
+    HIP_TRY(hipMemcpyAsync(rb->rt + slot, t + done, run * 4, hipMemcpyHostToDevice, rb->stream));
+    done += run;
+  }
+}
+
+static void replay_flush(ddpg_replay* rb) {
+  if (rb->st_n == 0) return;
+  ring_write(rb, rb->st_first, rb->st_n, rb->st_s.data(), rb->st_a.data(), rb->st_r.data(),
+             rb->st_t.data(), rb->st_s2.data());
+  HIP_TRY(hipStreamSynchronize(rb->stream));  // staging is reused after this
+  rb->st_n = 0;
+}
+
+int ddpg_replay_add(ddpg_replay* rb, const float* s, const float* a, const float* r,
+                    const uint8_t* t, const float* s2, int n) {
+  return rguard(rb, [&] {
+    if (n < 0) throw einval("negative row count");
+    HIP_TRY(hipSetDevice(rb->device));
+    const size_t S = rb->S, A = rb->A;
+    int done = 0;
+    while (done < n) {
+      if (rb->st_n == 0) rb->st_first = rb->total;
+      const int take = std::min(n - done, kStageRows - rb->st_n);
+      memcpy(rb->st_s.data() + rb->st_n * S, s + done * S, take * S * 4);
+      memcpy(rb->st_s2.data() + rb->st_n * S, s2 + done * S, take * S * 4);
+      memcpy(rb->st_a.data() + rb->st_n * A, a + done * A, take * A * 4);
+      for (int i = 0; i < take; ++i) {
+        rb->st_r[rb->st_n + i] = r[done + i];
+        rb->st_t[rb->st_n + i] = t[done + i] ? 1.f : 0.f;
+      }
+      rb->st_n += take;
+      rb->total += take;
+      rb->count = std::min<int64_t>(rb->total, rb->cap);
+      done += take;
+      if (rb->st_n == kStageRows) replay_flush(rb);
+    }
+  });
+}
+
+int64_t ddpg_replay_size(ddpg_replay* rb) { return rb ? rb->count : 0; }
+int64_t ddpg_replay_total_added(ddpg_replay* rb) { return rb ? rb->total : 0; }
+
+int ddpg_replay_clear(ddpg_replay* rb) {
+  return rguard(rb, [&] {
+    HIP_TRY(hipStreamSynchronize(rb->stream));
+    rb->count = rb->total = 0;
+    rb->st_n = 0;
+  });
+}
+
+// deque position -> ring slot (deque holds insertions [total-count, total))
+static inline int pos_to_slot(const ddpg_replay* rb, int64_t pos) {
+  return (int)((rb->total - rb->count + pos) % rb->cap);
+}
+
+int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* r, uint8_t* t,
+                             float* s2, int64_t* idx_out) {
+  int got = 0;
+  int rc = rguard(rb, [&] {
+    if (B < 0) throw einval("negative batch");
+    HIP_TRY(hipSetDevice(rb->device));
+    replay_flush(rb);
+    const int k = (int)std::min<int64_t>(B, rb->count);  // replay_buffer.py:36-39
+    rb->tmp_idx.resize(std::max(1, k));
+    if (rb->sampler.sample(rb->count, k, rb->tmp_idx.data()) != 0) throw einval("sample failed");
+    got = k;
+    if (idx_out) memcpy(idx_out, rb->tmp_idx.data(), k * sizeof(int64_t));
+    if (k == 0) return;
+    rb->tmp_slot.resize(k);
+    for (int i = 0; i < k; ++i) rb->tmp_slot[i] = pos_to_slot(rb, rb->tmp_idx[i]);
+    const int S = rb->S, A = rb->A;
+    if (rb->d_slots_cap < k) {
+      if (rb->d_slots) HIP_TRY(hipFree(rb->d_slots));
+      HIP_TRY(hipMalloc(&rb->d_slots, k * sizeof(int)));
+      rb->d_slots_cap = k;
+    }
+    const size_t need = (size_t)k * (2 * S + A + 2);
+    if (rb->d_tmp_cap < need) {
+      if (rb->d_tmp) HIP_TRY(hipFree(rb->d_tmp));
+      HIP_TRY(hipMalloc(&rb->d_tmp, need * 4));
+      rb->d_tmp_cap = need;
+    }
+    float* ds = rb->d_tmp;
+    float* ds2 = ds + (size_t)k * S;
+    float* da = ds2 + (size_t)k * S;
+    float* dr = da + (size_t)k * A;
+    float* dt = dr + k;
+    HIP_TRY(hipMemcpyAsync(rb->d_slots, rb->tmp_slot.data(), k * sizeof(int),
+                           hipMemcpyHostToDevice, rb->stream));
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(k, 4)), dim3(256), 0, rb->stream,
+                       rb->d_slots, k, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, S, A, ds, ds2, S,
+                       da, A, dr, dt, nullptr, nullptr);
+    HIP_TRY(hipGetLastError());
+    std::vector<float> tmp(need);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), rb->d_tmp, need * 4, hipMemcpyDeviceToHost, rb->stream));
+    HIP_TRY(hipStreamSynchronize(rb->stream));
+    if (s) memcpy(s, tmp.data(), (size_t)k * S * 4);
+    if (s2) memcpy(s2, tmp.data() + (size_t)k * S, (size_t)k * S * 4);
+    if (a) memcpy(a, tmp.data() + (size_t)2 * k * S, (size_t)k * A * 4);
+    if (r) memcpy(r, tmp.data() + (size_t)k * (2 * S + A), (size_t)k * 4);
+    if (t)
+      for (int i = 0; i < k; ++i) t[i] = tmp[(size_t)k * (2 * S + A + 1) + i] != 0.f;
+  });
+  return rc == DDPG_OK ? got : rc;
+}
+
+// ---------------------------------------------------------------- fused step
+static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg,
+                        ddpg_stats* stats) {
+  if (rb->S != c->S || rb->A != c->A)
+    throw einval("replay dims (S=%d, A=%d) != network dims (S=%d, A=%d)", rb->S, rb->A, c->S,
+                 c->A);
+  if (Bg % c->world) throw einval("global batch %d not divisible by world %d", Bg, c->world);
+  const int B = Bg / c->world;
+  check_b(c, B);
+  // this rank's slice of the globally drawn positions -> ring slots (pinned)
+  const int si = c->slot_i;
+  c->slot_i = (c->slot_i + 1) % kSlotRing;
+  HIP_TRY(hipEventSynchronize(c->slot_ev[si]));
+  int* hs = c->h_slots + (size_t)si * c->Bmax;
+  const int64_t* mine = idx + (size_t)c->rank * B;
+  for (int i = 0; i < B; ++i) hs[i] = pos_to_slot(rb, mine[i]);
+  HIP_TRY(hipMemcpyAsync(c->d_slots, hs, (size_t)B * sizeof(int), hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
+  {
+    ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->stream,
+                       c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, c->S, c->A, c->s,
+                       c->s2, c->ldS, c->a, c->ldA, c->r, c->t,
+                       c->has_scaler ? c->dmean : nullptr, c->has_scaler ? c->dscale : nullptr);
+    HIP_TRY(hipGetLastError());
+  }
+  learner_step_dev(c, B, 1.0f / (float)Bg);
+  if (stats) {
+    float st[2];
+    HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    stats->q_max = st[0];
+    stats->loss = st[1];
+  }
+}
+
+int ddpg_learner_step(ddpg_ctx* c, ddpg_replay* rb, int Bg, ddpg_stats* stats) {
+  return guard(c, [&] {
+    if (!rb) throw einval("null replay");
+    replay_flush(rb);
+    if (rb->count < Bg) throw einval("replay holds %lld rows < batch %d", (long long)rb->count, Bg);
+    c->idx_tmp.resize(Bg);
+    if (rb->sampler.sample(rb->count, Bg, c->idx_tmp.data()) != 0) throw einval("sample failed");
+    step_common(c, rb, c->idx_tmp.data(), Bg, stats);
+  });
+}
+
+int ddpg_learner_step_indices(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg,
+                              ddpg_stats* stats) {
+  return guard(c, [&] {
+    if (!rb || !idx) throw einval("null argument");
+    replay_flush(rb);
+    for (int i = 0; i < Bg; ++i)
+      if (idx[i] < 0 || idx[i] >= rb->count) throw einval("index %lld out of range", (long long)idx[i]);
+    step_common(c, rb, idx, Bg, stats);
+  });
+}
+
+int ddpg_read_stats(ddpg_ctx* c, double* qsum, double* lsum, int64_t* steps, int reset) {
+  return guard(c, [&] {
+    double acc[4];
+    HIP_TRY(hipMemcpyAsync(acc, c->dacc, sizeof acc, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (qsum) *qsum = acc[0];
+    if (lsum) *lsum = acc[1];
+    if (steps) *steps = (int64_t)acc[2];
+    if (reset) HIP_TRY(hipMemsetAsync(c->dacc, 0, 4 * sizeof(double), c->stream));
+  });
+}
+
+// ---------------------------------------------------------------- comm
+int ddpg_comm_unique_id(char* out128) {
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    g_err = ncclGetErrorString(r);
+    return DDPG_ECOMM;
+  }
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  memcpy(out128, &id, 128);
+  return DDPG_OK;
+}
+
+int ddpg_comm_init(ddpg_ctx* c, const char* id128, int world, int rank) {
+  return guard(c, [&] {
+    if (world != c->world || rank != c->rank)
+      throw einval("comm (%d/%d) != cfg (%d/%d)", rank, world, c->rank, c->world);
+    if (world <= 1) return;
+    ncclUniqueId id;
+    memcpy(&id, id128, 128);
+    HIP_TRY(hipSetDevice(c->cfg.device));
+    ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
+  });
+}
+
+// ---------------------------------------------------------------- profiling
+int ddpg_profile_enable(ddpg_ctx* c, int enable) {
+  return guard(c, [&] {
+    prof_collect(c);
+    c->prof_agg.clear();
+    c->prof = enable != 0;
+  });
+}
+
+int ddpg_profile_read(ddpg_ctx* c, int n, char (*names)[64], double* ms, int64_t* launches,
+                      double* flops, double* bytes) {
+  int count = 0;
+  int rc = guard(c, [&] {
+    prof_collect(c);
+    for (auto& kv : c->prof_agg) {
+      if (count >= n) break;
+      snprintf(names[count], 64, "%s", kv.first.c_str());
+      ms[count] = kv.second.ms;
+      launches[count] = kv.second.launches;
+      flops[count] = kv.second.flops;
+      bytes[count] = kv.second.bytes;
+      ++count;
+    }
+  });
+  return rc == DDPG_OK ? count : rc;
+}
+
+}  // extern "C"

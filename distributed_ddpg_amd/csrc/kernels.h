@@ -1,0 +1,299 @@
+// Memory-bound kernels of the learner step (gfx950): replay gather (K8),
+// thin-head finalisers (K1/K2/K4 epilogue reductions, K9 TD target), critic
+// head backward, split-K / partial-sum reduction, TF ApplyAdam (K6) and the
+// tau soft update (K7).  All fp32; rounding mirrors the TF 1.3 CPU kernels
+// (no FMA contraction where TF evaluates separate multiplies and adds).
+#pragma once
+#include "common.h"
+
+namespace ddpg {
+
+// ---------------------------------------------------------------- K8 gather
+// replay_buffer.py:41-45 (np.array stacking of the sampled tuples), from a
+// device-resident SoA ring.  One wave per row; lanes stride the features.
+// Optional scaler (networks.py:65-69): fp32((double(x) - mean) / scale).
+__global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
+                                   const float* __restrict__ rs, const float* __restrict__ ra,
+                                   const float* __restrict__ rr, const float* __restrict__ rt,
+                                   const float* __restrict__ rs2, int S, int A,
+                                   float* __restrict__ s, float* __restrict__ s2, int lds,
+                                   float* __restrict__ a, int lda, float* __restrict__ r,
+                                   float* __restrict__ t, const double* __restrict__ mean,
+                                   const double* __restrict__ scale) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int b = wave; b < B; b += nwaves) {
+    const size_t slot = (size_t)slots[b];
+    const float* ps = rs + slot * S;
+    const float* ps2 = rs2 + slot * S;
+    for (int j = lane; j < S; j += 64) {
+      float x = ps[j], x2 = ps2[j];
+      if (mean) {
+        x = (float)(((double)x - mean[j]) / scale[j]);
+        x2 = (float)(((double)x2 - mean[j]) / scale[j]);
+      }
+      s[(size_t)b * lds + j] = x;
+      s2[(size_t)b * lds + j] = x2;
+    }
+    for (int j = lane; j < A; j += 64) a[(size_t)b * lda + j] = ra[slot * A + j];
+    if (lane == 0) {
+      r[b] = rr[slot];
+      t[b] = rt[slot];
+    }
+  }
+}
+
+// Apply the scaler in place to a [B][ld] state buffer (1:1 API path).
+__global__ void scale_rows_kernel(float* __restrict__ x, int B, int S, int ld,
+                                  const double* __restrict__ mean,
+                                  const double* __restrict__ scale) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * S) return;
+  const int b = i / S, j = i - b * S;
+  float* p = x + (size_t)b * ld + j;
+  *p = (float)(((double)*p - mean[j]) / scale[j]);
+}
+
+// ---------------------------------------------------------------- thin heads
+// actor output: o = tanh(sum_t part[t][b][a]); mu = o * scale  (networks.py:59-61)
+__global__ void actor_out_kernel(const float* __restrict__ part, int NT, int B, int A,
+                                 float scale, float* __restrict__ o, float* __restrict__ mu,
+                                 int ld) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * A) return;
+  const int b = i / A, a = i - b * A;
+  float z = 0.f;
+  for (int tt = 0; tt < NT; ++tt) z += part[((size_t)tt * B + b) * A + a];
+  const float ov = tanhf(z);
+  if (o) o[(size_t)b * ld + a] = ov;
+  if (mu) mu[(size_t)b * ld + a] = __fmul_rn(ov, scale);
+}
+
+// critic output q = sum_t qpart[t][b] + bo, then by mode:
+//   mode 0: q only;  mode 1: TD target y = t ? r : r + gamma*q  (ddpg.py:92-100)
+__global__ void critic_q_kernel(const float* __restrict__ qpart, int NT, int B,
+                                const float* __restrict__ bo, float* __restrict__ q,
+                                int mode, const float* __restrict__ r,
+                                const float* __restrict__ t, float gamma,
+                                float* __restrict__ y) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float z = 0.f;
+  for (int tt = 0; tt < NT; ++tt) z += qpart[(size_t)tt * B + b];
+  z = __fadd_rn(z, bo[0]);
+  if (q) q[b] = z;
+  if (mode == 1) y[b] = (t[b] != 0.f) ? r[b] : __fadd_rn(r[b], __fmul_rn(gamma, z));
+}
+
+// Critic train head (networks.py:136, tflearn.mean_square): q = sum + bo,
+// L = mean((y - q)^2), dq = -((1/B) * (2 * (y - q))).  Single block; also
+// writes per-step stats {q_max, loss} and accumulates them.
+// inv_b is 1/B_global; the loss written is this rank's share of the mean.
+__global__ void critic_loss_kernel(const float* __restrict__ qpart, int NT, int B,
+                                   const float* __restrict__ bo, const float* __restrict__ y,
+                                   float inv_b, float* __restrict__ q, float* __restrict__ dq,
+                                   float* __restrict__ stats /* [q_max, loss] */,
+                                   double* __restrict__ acc /* [qmax_sum, loss_sum, steps] */) {
+  __shared__ float s_sum[1024];
+  __shared__ float s_max[1024];
+  float lsum = 0.f, lmax = -INFINITY;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    float z = 0.f;
+    for (int tt = 0; tt < NT; ++tt) z += qpart[(size_t)tt * B + b];
+    z = __fadd_rn(z, bo[0]);
+    q[b] = z;
+    const float d = __fsub_rn(y[b], z);
+    dq[b] = -__fmul_rn(inv_b, __fmul_rn(2.f, d));
+    lsum += __fmul_rn(d, d);
+    lmax = fmaxf(lmax, z);
+  }
+  s_sum[threadIdx.x] = lsum;
+  s_max[threadIdx.x] = lmax;
+  __syncthreads();
+  for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
+      s_max[threadIdx.x] = fmaxf(s_max[threadIdx.x], s_max[threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float loss = __fmul_rn(s_sum[0], inv_b);
+    stats[0] = s_max[0];
+    stats[1] = loss;
+    if (acc) {
+      acc[0] += (double)s_max[0];
+      acc[1] += (double)loss;
+      acc[2] += 1.0;
+    }
+  }
+}
+
+// Critic head backward (gradients_1 of networks.py:137):
+//   dh[b,j] = dq[b]*Wo[j];  dh_pre = EluGrad(dh, h);  dWo[j] = sum_b h*dq;
+//   dbh[j] = sum_b dh_pre;  dbo = sum_b dq.   Partial sums per row chunk.
+__global__ void critic_head_bwd_kernel(const float* __restrict__ h, int ldh,
+                                       const float* __restrict__ dq,
+                                       const float* __restrict__ Wo, int B, int H2,
+                                       int rows_per_chunk, float* __restrict__ dh_pre,
+                                       int ld_dh, float* __restrict__ part_dWo,
+                                       float* __restrict__ part_dbh,
+                                       float* __restrict__ part_dbo) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int chunk = blockIdx.y;
+  const int b0 = chunk * rows_per_chunk;
+  const int b1 = min(B, b0 + rows_per_chunk);
+  if (j < H2) {
+    const float w = Wo[j];
+    float sw = 0.f, sb = 0.f;
+    for (int b = b0; b < b1; ++b) {
+      const float hv = h[(size_t)b * ldh + j];
+      const float d = dq[b];
+      const float dp = __fmul_rn(__fmul_rn(d, w), elu_grad_factor(hv));
+      dh_pre[(size_t)b * ld_dh + j] = dp;
+      sw = fmaf(hv, d, sw);
+      sb += dp;
+    }
+    part_dWo[(size_t)chunk * H2 + j] = sw;
+    part_dbh[(size_t)chunk * H2 + j] = sb;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = b0; b < b1; ++b) s += dq[b];
+    part_dbo[chunk] = s;
+  }
+}
+
+// dQ/da finaliser (networks.py:143 action half) + actor grad_ys
+// (networks.py:44): da = sum_t part[t][b][a];
+// dz3 = TanhGrad(o, (-da) * scale) = ((-da)*scale) * (1 - o*o).
+__global__ void action_grad_kernel(const float* __restrict__ part, int NT, int B, int A,
+                                   int ld_part_b /* rows stride inside a tile slab = B */,
+                                   const float* __restrict__ o, int ld, float scale,
+                                   float* __restrict__ da, float* __restrict__ dz3) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * A) return;
+  const int b = i / A, a = i - b * A;
+  float g = 0.f;
+  for (int tt = 0; tt < NT; ++tt) g += part[((size_t)tt * ld_part_b + b) * A + a];
+  if (da) da[(size_t)b * ld + a] = g;
+  if (dz3) {
+    const float ov = o[(size_t)b * ld + a];
+    const float dy = __fmul_rn(-g, scale);
+    dz3[(size_t)b * ld + a] = __fmul_rn(dy, __fsub_rn(1.f, __fmul_rn(ov, ov)));
+  }
+}
+
+// ---------------------------------------------------------------- reductions
+struct ReduceSeg {
+  const float* src;
+  float* dst;
+  long long slab_stride;  // floats between slabs
+  int nslab;
+  int rows, cols;         // dst region [rows][cols] (contiguous)
+  int src_ld;             // row stride inside a slab
+};
+constexpr int MAX_SEGS = 12;
+struct ReduceTable {
+  ReduceSeg seg[MAX_SEGS];
+  long long start[MAX_SEGS + 1];
+  int nseg;
+};
+
+// dst = sum over slabs (deterministic order).
+__global__ void reduce_slabs_kernel(ReduceTable tab) {
+  const long long total = tab.start[tab.nseg];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int s = 0;
+    while (i >= tab.start[s + 1]) ++s;
+    const ReduceSeg& g = tab.seg[s];
+    const long long li = i - tab.start[s];
+    const int row = (int)(li / g.cols), col = (int)(li - (long long)row * g.cols);
+    const float* p = g.src + (size_t)row * g.src_ld + col;
+    float acc = 0.f;
+    for (int k = 0; k < g.nslab; ++k) acc += p[(size_t)k * g.slab_stride];
+    g.dst[li] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- K6 Adam
+// TF 1.3 ApplyAdam (use_nesterov = false), one flat pass per network:
+//   alpha = lr * sqrt(1 - b2p) / (1 - b1p)
+//   m += (g - m) * (1 - b1);  v += (g*g - v) * (1 - b2)
+//   p -= (m * alpha) / (sqrt(v) + eps)
+// The beta powers live on device (pw = {b1p, b2p}); the last block to finish
+// advances them (b1p *= b1, b2p *= b2), i.e. the AdamOptimizer._finish update.
+__global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
+                            float* __restrict__ v, const float* __restrict__ g, long long n,
+                            float* __restrict__ pw, unsigned* __restrict__ counter, float lr,
+                            float b1, float b2, float eps) {
+  const float b1p = pw[0], b2p = pw[1];
+  const float alpha = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.f, b2p))),
+                                __fsub_rn(1.f, b1p));
+  const float omb1 = __fsub_rn(1.f, b1), omb2 = __fsub_rn(1.f, b2);
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 P = reinterpret_cast<float4*>(p)[i];
+    float4 Mv = reinterpret_cast<float4*>(m)[i];
+    float4 V = reinterpret_cast<const float4*>(v)[i];
+    const float4 G = reinterpret_cast<const float4*>(g)[i];
+    float* pp = &P.x;
+    float* pm = &Mv.x;
+    float* pv = &V.x;
+    const float* pg = &G.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pm[k] = __fadd_rn(pm[k], __fmul_rn(__fsub_rn(pg[k], pm[k]), omb1));
+      pv[k] = __fadd_rn(pv[k], __fmul_rn(__fsub_rn(__fmul_rn(pg[k], pg[k]), pv[k]), omb2));
+      pp[k] = __fsub_rn(pp[k], __fdiv_rn(__fmul_rn(pm[k], alpha),
+                                         __fadd_rn(__fsqrt_rn(pv[k]), eps)));
+    }
+    reinterpret_cast<float4*>(p)[i] = P;
+    reinterpret_cast<float4*>(m)[i] = Mv;
+    reinterpret_cast<float4*>(v)[i] = V;
+  }
+  // tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long i = (n4 << 2) + threadIdx.x;
+    m[i] = __fadd_rn(m[i], __fmul_rn(__fsub_rn(g[i], m[i]), omb1));
+    v[i] = __fadd_rn(v[i], __fmul_rn(__fsub_rn(__fmul_rn(g[i], g[i]), v[i]), omb2));
+    p[i] = __fsub_rn(p[i], __fdiv_rn(__fmul_rn(m[i], alpha), __fadd_rn(__fsqrt_rn(v[i]), eps)));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(counter, 1u);
+    if (prev == gridDim.x - 1) {
+      pw[0] = __fmul_rn(b1p, b1);
+      pw[1] = __fmul_rn(b2p, b2);
+      atomicExch(counter, 0u);
+      __threadfence();
+    }
+  }
+}
+
+// ---------------------------------------------------------------- K7 soft update
+// networks.py:34-37: target.assign(theta * tau + target * (1. - tau)), fp32.
+__global__ void soft_update_kernel(const float* __restrict__ th, float* __restrict__ tt,
+                                   long long n, float tau, float omt) {
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(th)[i];
+    float4 b = reinterpret_cast<float4*>(tt)[i];
+    b.x = __fadd_rn(__fmul_rn(a.x, tau), __fmul_rn(b.x, omt));
+    b.y = __fadd_rn(__fmul_rn(a.y, tau), __fmul_rn(b.y, omt));
+    b.z = __fadd_rn(__fmul_rn(a.z, tau), __fmul_rn(b.z, omt));
+    b.w = __fadd_rn(__fmul_rn(a.w, tau), __fmul_rn(b.w, omt));
+    reinterpret_cast<float4*>(tt)[i] = b;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long i = (n4 << 2) + threadIdx.x;
+    tt[i] = __fadd_rn(__fmul_rn(th[i], tau), __fmul_rn(tt[i], omt));
+  }
+}
+
+}  // namespace ddpg

@@ -1,0 +1,327 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the CPU oracle.
+
+Tolerances (BASELINE.json north_star), measured as max|x - ref| / max|ref|
+over each tensor:
+  forward outputs                          1e-5
+  gradients / parameters / Adam slots      1e-4 (fp32), after N steps
+  soft update                              bit-exact (same fp32 ops as TF)
+  replay indices / gathered rows           bit-exact
+The oracle runs in float64 on the same fp32 inputs and weights.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+FWD_TOL = 1e-5
+GRAD_TOL = 1e-4
+
+
+def rel(x, ref):
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert x.shape == ref.shape, (x.shape, ref.shape)
+    den = max(np.max(np.abs(ref)), 1e-30)
+    return float(np.max(np.abs(x - ref)) / den)
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ddpg_oracle
+    return ddpg_oracle
+
+
+@pytest.fixture(scope="module")
+def dd():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import distributed_ddpg_amd.networks as nets
+    return nets
+
+
+CONFIGS = {
+    # name: S, A, H1, H2, scale, B, source
+    "ip": (4, 1, 128, 200, 3.0, 64, "ip_model1410"),
+    "mc": (2, 1, 48, 64, 1.0, 64, "mc_model120"),
+    "odd": (5, 3, 40, 72, 2.0, 37, None),
+    "wide": (64, 16, 1024, 1024, 1.0, 256, None),
+}
+
+
+def _params(O, name):
+    S, A, H1, H2, scale, B, src = CONFIGS[name]
+    if src:
+        z = np.load(os.path.join(GOLD, src + ".npz"))
+        get = lambda names, keys: {k: z[n].astype(np.float32) for k, n in zip(keys, names)}
+        p = {"actor": get(O.CKPT_ACTOR, O.ACTOR_KEYS), "actor_t": get(O.CKPT_ACTOR_T, O.ACTOR_KEYS),
+             "critic": get(O.CKPT_CRITIC, O.CRITIC_KEYS),
+             "critic_t": get(O.CKPT_CRITIC_T, O.CRITIC_KEYS)}
+        return p, z
+    a, c = O.init_params(S, A, H1, H2, seed=11)
+    at, ct = O.init_params(S, A, H1, H2, seed=12)
+    # larger-than-init weights so every branch (elu < 0, tanh saturation) is exercised
+    rng = np.random.default_rng(3)
+    for d in (a, c, at, ct):
+        for k in d:
+            d[k] = (d[k] + rng.standard_normal(d[k].shape).astype(np.float32) * 0.05).astype(
+                np.float32)
+    return {"actor": a, "actor_t": at, "critic": c, "critic_t": ct}, None
+
+
+def _session(dd, O, name, p, batch_max=4096):
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    from distributed_ddpg_amd import _lib
+    dd.reset_default_graph()
+    actor = dd.ActorNetwork(S, A, scale, 1e-4, 1e-3, None, h1=H1, h2=H2)
+    critic = dd.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), None, h1=H1, h2=H2)
+    sess = dd.Session(batch_max=batch_max)
+    actor.set_session(sess)
+    critic.set_session(sess)
+    sess.set_params(_lib.ACTOR, [p["actor"][k] for k in O.ACTOR_KEYS])
+    sess.set_params(_lib.ACTOR_TARGET, [p["actor_t"][k] for k in O.ACTOR_KEYS])
+    sess.set_params(_lib.CRITIC, [p["critic"][k] for k in O.CRITIC_KEYS])
+    sess.set_params(_lib.CRITIC_TARGET, [p["critic_t"][k] for k in O.CRITIC_KEYS])
+    return sess, actor, critic
+
+
+def _batch(name, seed=0, B=None):
+    S, A, H1, H2, scale, B0, _ = CONFIGS[name]
+    B = B or B0
+    rng = np.random.default_rng(seed)
+    s = rng.standard_normal((B, S)).astype(np.float32)
+    a = (rng.uniform(-1, 1, (B, A)) * scale).astype(np.float32)
+    return s, a, rng
+
+
+def f64(d):
+    return {k: v.astype(np.float64) for k, v in d.items()}
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_forward_parity(dd, O, name):
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    sess, actor, critic = _session(dd, O, name, p)
+    s, a, _ = _batch(name)
+    for Bq in (1, B):
+        mu = actor.predict(s[:Bq])
+        assert mu.dtype == np.float32 and mu.shape == (Bq, A)
+        ref = O.actor_forward(f64(p["actor"]), s[:Bq].astype(np.float64), scale)[3]
+        assert rel(mu, ref) < FWD_TOL
+        mut = actor.predict_target(s[:Bq])
+        assert rel(mut, O.actor_forward(f64(p["actor_t"]), s[:Bq].astype(np.float64), scale)[3]) < FWD_TOL
+        q = critic.predict(s[:Bq], a[:Bq])
+        assert q.shape == (Bq, 1)
+        assert rel(q, O.critic_forward(f64(p["critic"]), s[:Bq].astype(np.float64),
+                                       a[:Bq].astype(np.float64))[3]) < FWD_TOL
+        qt = critic.predict_target(s[:Bq], a[:Bq])
+        assert rel(qt, O.critic_forward(f64(p["critic_t"]), s[:Bq].astype(np.float64),
+                                        a[:Bq].astype(np.float64))[3]) < FWD_TOL
+    sess.close()
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_train_methods_parity(dd, O, name):
+    """critic.train -> action_gradients -> actor.train, 3 rounds, vs oracle."""
+    from distributed_ddpg_amd import _lib
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    sess, actor, critic = _session(dd, O, name, p)
+    L = O.Learner(S, A, H1, H2, scale, actor_lr=1e-4, critic_lr=1e-3, tau=1e-3,
+                  dtype=np.float64, params=p, init_blend=False)
+    for it in range(3):
+        s, a, rng = _batch(name, seed=10 + it)
+        y = rng.standard_normal((B, 1)).astype(np.float32)
+        q, none, loss = critic.train(s, a, y)
+        assert none is None and q.shape == (B, 1) and q.dtype == np.float32
+        q_ref, loss_ref, _ = L.critic_train(s.astype(np.float64), a.astype(np.float64),
+                                            y.astype(np.float64))
+        assert rel(q, q_ref) < FWD_TOL
+        assert abs(float(loss) - loss_ref) <= GRAD_TOL * abs(loss_ref)
+        a_out = actor.predict(s)
+        a_ref = L.actor_predict(s.astype(np.float64))
+        assert rel(a_out, a_ref) < FWD_TOL
+        (da,) = critic.action_gradients(s, a_out)
+        da_ref = L.action_gradients(s.astype(np.float64), a_out.astype(np.float64))
+        assert rel(da, da_ref) < GRAD_TOL
+        actor.train(s, da)
+        L.actor_train(s.astype(np.float64), da.astype(np.float64))
+    got_c = sess.get_params(_lib.CRITIC)
+    got_a = sess.get_params(_lib.ACTOR)
+    for k, v in zip(O.CRITIC_KEYS, got_c):
+        assert rel(v, L.critic[k].reshape(v.shape)) < GRAD_TOL, ("critic", k)
+    for k, v in zip(O.ACTOR_KEYS, got_a):
+        assert rel(v, L.actor[k].reshape(v.shape)) < GRAD_TOL, ("actor", k)
+    for which, opt, keys in ((_lib.CRITIC_ADAM_M, L.critic_opt.m, O.CRITIC_KEYS),
+                             (_lib.CRITIC_ADAM_V, L.critic_opt.v, O.CRITIC_KEYS),
+                             (_lib.ACTOR_ADAM_M, L.actor_opt.m, O.ACTOR_KEYS),
+                             (_lib.ACTOR_ADAM_V, L.actor_opt.v, O.ACTOR_KEYS)):
+        for k, v in zip(keys, sess.get_params(which)):
+            assert rel(v, opt[k].reshape(v.shape)) < GRAD_TOL, (which, k)
+    b1p, b2p = sess.get_adam_powers(1)
+    assert b1p == np.float32(0.9) ** 4 or abs(b1p - 0.9 ** 4) < 1e-7
+    assert abs(b2p - 0.999 ** 4) < 1e-6
+    sess.close()
+
+
+def test_soft_update_bitexact(dd, O):
+    from distributed_ddpg_amd import _lib
+    p, _ = _params(O, "odd")
+    sess, actor, critic = _session(dd, O, "odd", p)
+    for _ in range(2):
+        actor.update_target_network()
+    critic.update_target_network()
+    tau, omt = np.float32(0.001), np.float32(0.999)
+    exp_a = {k: p["actor_t"][k].copy() for k in O.ACTOR_KEYS}
+    for _ in range(2):
+        exp_a = {k: (p["actor"][k] * tau + exp_a[k] * omt).astype(np.float32) for k in exp_a}
+    exp_c = {k: (p["critic"][k] * tau + p["critic_t"][k] * omt).astype(np.float32)
+             for k in O.CRITIC_KEYS}
+    for k, v in zip(O.ACTOR_KEYS, sess.get_params(_lib.ACTOR_TARGET)):
+        assert np.array_equal(v, exp_a[k].reshape(v.shape)), k
+    for k, v in zip(O.CRITIC_KEYS, sess.get_params(_lib.CRITIC_TARGET)):
+        assert np.array_equal(v, exp_c[k].reshape(v.shape)), k
+    sess.close()
+
+
+def test_mc_checkpoint_adam_resume(dd, O):
+    """Resume from the reference's MountainCar checkpoint mid-run (t ~ 45k
+    Adam steps, non-trivial bias correction): restore weights, Adam slots and
+    beta powers, do one critic/actor update, compare with the oracle."""
+    from distributed_ddpg_amd import _lib
+    p, z = _params(O, "mc")
+    S, A, H1, H2, scale, B, _ = CONFIGS["mc"]
+    sess, actor, critic = _session(dd, O, "mc", p)
+    slots = lambda names, suf: [z[n + suf] for n in names]
+    sess.set_params(_lib.ACTOR_ADAM_M, slots(O.CKPT_ACTOR, "/Adam"))
+    sess.set_params(_lib.ACTOR_ADAM_V, slots(O.CKPT_ACTOR, "/Adam_1"))
+    sess.set_params(_lib.CRITIC_ADAM_M, slots(O.CKPT_CRITIC, "/Adam"))
+    sess.set_params(_lib.CRITIC_ADAM_V, slots(O.CKPT_CRITIC, "/Adam_1"))
+    sess.set_adam_powers(0, float(z["beta1_power"]), float(z["beta2_power"]))
+    sess.set_adam_powers(1, float(z["beta1_power_1"]), float(z["beta2_power_1"]))
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    for net, names in ((L.actor_opt, O.CKPT_ACTOR), (L.critic_opt, O.CKPT_CRITIC)):
+        keys = O.ACTOR_KEYS if names is O.CKPT_ACTOR else O.CRITIC_KEYS
+        for k, n in zip(keys, names):
+            net.m[k] = z[n + "/Adam"].astype(np.float64)
+            net.v[k] = z[n + "/Adam_1"].astype(np.float64)
+    L.actor_opt.b1p, L.actor_opt.b2p = np.float64(z["beta1_power"]), np.float64(z["beta2_power"])
+    L.critic_opt.b1p, L.critic_opt.b2p = (np.float64(z["beta1_power_1"]),
+                                          np.float64(z["beta2_power_1"]))
+    s, a, rng = _batch("mc", seed=5)
+    y = rng.standard_normal((B, 1)).astype(np.float32)
+    critic.train(s, a, y)
+    L.critic_train(s.astype(np.float64), a.astype(np.float64), y.astype(np.float64))
+    da = rng.standard_normal((B, A)).astype(np.float32)
+    actor.train(s, da)
+    L.actor_train(s.astype(np.float64), da.astype(np.float64))
+    for k, v in zip(O.CRITIC_KEYS, sess.get_params(_lib.CRITIC)):
+        assert rel(v, L.critic[k].reshape(v.shape)) < GRAD_TOL, k
+    for k, v in zip(O.ACTOR_KEYS, sess.get_params(_lib.ACTOR)):
+        assert rel(v, L.actor[k].reshape(v.shape)) < GRAD_TOL, k
+    sess.close()
+
+
+def _fill(rb, S, A, n, scale, seed):
+    rng = np.random.default_rng(seed)
+    s = rng.standard_normal((n, S)).astype(np.float32)
+    s2 = rng.standard_normal((n, S)).astype(np.float32)
+    a = (rng.uniform(-1, 1, (n, A)) * scale).astype(np.float32)
+    r = rng.standard_normal(n).astype(np.float32)
+    t = rng.random(n) < 0.05
+    rb.add_batch(s, a, r, t, s2)
+    return s, a, r, t, s2
+
+
+def test_replay_device_sample_bitexact(dd):
+    """Device ring + host sampler reproduce the reference's index streams
+    (golden fixture cases) and return exactly the inserted rows."""
+    import json
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    z = np.load(os.path.join(GOLD, "replay_indices.npz"))
+    cases = {c["name"]: c for c in json.loads(bytes(z["__cases__"]).decode())}
+    for name in ("survey_prewrap", "survey_postwrap", "interleaved_wrap", "count_lt_batch",
+                 "pool_branch_b256", "full_1e6_b4096"):
+        c = cases[name]
+        rb = ReplayBuffer(c["capacity"], c["seed"])
+        total, j = 0, 0
+        for op, n in c["ops"]:
+            if op == "add":
+                ids = np.arange(total, total + n)
+                rb.add_batch(ids[:, None].astype(np.float32) % 1e7, np.zeros((n, 1), np.float32),
+                             (ids * 0.5).astype(np.float32), ids % 7 == 0,
+                             (ids[:, None] % 1e7).astype(np.float32))
+                total += n
+            else:
+                s, a, r, t, s2, idx = rb.sample_batch(n, return_indices=True)
+                exp = z["%s__%d" % (name, j)]
+                ins = (total - rb.size()) + idx
+                assert np.array_equal(ins, exp), name
+                assert np.array_equal(s[:, 0], (exp % 10_000_000).astype(np.float64)), name
+                assert np.array_equal(r, (exp * 0.5).astype(np.float32).astype(np.float64))
+                assert np.array_equal(t, exp % 7 == 0)
+                assert s.dtype == np.float64 and a.dtype == np.float32 and t.dtype == bool
+                j += 1
+
+
+@pytest.mark.parametrize("name", ["ip", "odd", "wide"])
+def test_fused_learner_step_parity(dd, O, name):
+    """ddpg_learner_step (sample -> gather -> whole update on device) vs the
+    oracle's ddpg.py:86-113 sequence on the same sampled rows, 4 steps."""
+    import random
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    sess, actor, critic = _session(dd, O, name, p)
+    rb = ReplayBuffer(5000, 1234)
+    rows = _fill(rb, S, A, 3000, scale, seed=2)
+    fl = FusedLearner(sess, rb, B)
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    ref_rng = random.Random(1234)  # the reference's global RNG after random.seed(1234)
+    for it in range(4):
+        idx = np.array(ref_rng.sample(range(3000), B))
+        qmax, loss = fl.step(stats=True)
+        s, a, r, t, s2 = (x[idx] for x in rows)
+        out = L.step(s, a, r, t, s2)
+        assert abs(qmax - float(np.max(out["q"]))) <= FWD_TOL * max(1.0, abs(np.max(out["q"]))) * 10
+        assert abs(loss - float(out["loss"])) <= GRAD_TOL * abs(float(out["loss"]))
+    for which, ref, keys in ((_lib.ACTOR, L.actor, O.ACTOR_KEYS),
+                             (_lib.CRITIC, L.critic, O.CRITIC_KEYS),
+                             (_lib.ACTOR_TARGET, L.actor_t, O.ACTOR_KEYS),
+                             (_lib.CRITIC_TARGET, L.critic_t, O.CRITIC_KEYS)):
+        for k, v in zip(keys, sess.get_params(which)):
+            assert rel(v, ref[k].reshape(v.shape)) < GRAD_TOL, (which, k)
+    q_sum, l_sum, n = fl.read_stats()
+    assert n == 4
+    sess.close()
+
+
+def test_batch_4096_wide_step_properties(dd, O):
+    """Full C3 shape (S=64, A=16, 1024/1024, B=4096): one fused step equals
+    the oracle step on the same rows (fp64 oracle at full size)."""
+    import random
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale = 64, 16, 1024, 1024, 1.0
+    B = 4096
+    p, _ = _params(O, "wide")
+    sess, actor, critic = _session(dd, O, "wide", p, batch_max=B)
+    rb = ReplayBuffer(20000, 77)
+    rows = _fill(rb, S, A, 20000, scale, seed=9)
+    fl = FusedLearner(sess, rb, B)
+    idx = np.array(random.Random(77).sample(range(20000), B))
+    fl.step()
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    L.step(*(x[idx] for x in rows))
+    for which, ref, keys in ((_lib.ACTOR, L.actor, O.ACTOR_KEYS),
+                             (_lib.CRITIC, L.critic, O.CRITIC_KEYS)):
+        for k, v in zip(keys, sess.get_params(which)):
+            assert rel(v, ref[k].reshape(v.shape)) < GRAD_TOL, (which, k)
+    sess.close()
