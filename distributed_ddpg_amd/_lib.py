@@ -38,7 +38,8 @@ class Cfg(ctypes.Structure):
                 ("action_scale", ctypes.c_float), ("beta1", ctypes.c_float),
                 ("beta2", ctypes.c_float), ("epsilon", ctypes.c_float),
                 ("dtype", ctypes.c_int), ("device", ctypes.c_int),
-                ("rank", ctypes.c_int), ("world", ctypes.c_int)]
+                ("rank", ctypes.c_int), ("world", ctypes.c_int),
+                ("critic_h1", ctypes.c_int), ("critic_h2", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):

@@ -63,7 +63,7 @@ enum { CWS, CBS, CWA, CBA, CWH, CBH, CWO, CBO, NC };
 struct Layout {
   Tensor a[NA], c[NC];
   size_t actor_begin, actor_end, critic_begin, critic_end, total;
-  void build(int S, int A, int H1, int H2) {
+  void build(int S, int A, int H1, int H2, int CH1, int CH2) {
     size_t off = 0;
     auto place = [&](Tensor& t, int r, int c) {
       t.rows = r;
@@ -78,13 +78,13 @@ struct Layout {
     place(a[AB2], H2, 1);
     place(a[AW3], H2, A);
     actor_end = critic_begin = off;
-    place(c[CWS], S, H1);
-    place(c[CBS], H1, 1);
-    place(c[CWA], A, H1);
-    place(c[CBA], H1, 1);
-    place(c[CWH], 2 * H1, H2);
-    place(c[CBH], H2, 1);
-    place(c[CWO], H2, 1);
+    place(c[CWS], S, CH1);
+    place(c[CBS], CH1, 1);
+    place(c[CWA], A, CH1);
+    place(c[CBA], CH1, 1);
+    place(c[CWH], 2 * CH1, CH2);
+    place(c[CBH], CH2, 1);
+    place(c[CWO], CH2, 1);
     place(c[CBO], 1, 1);
     critic_end = total = off;
   }
@@ -128,8 +128,8 @@ static void replay_flush(ddpg_replay* rb);
 struct ddpg_ctx {
   ddpg_cfg cfg{};
   Layout L;
-  int S, A, H1, H2, Bmax;
-  int ldS, ldA, ldH1, ldH2, ldC;
+  int S, A, AH1, AH2, CH1, CH2, Bmax;
+  int ldS, ldA, ldAH1, ldAH2, ldCH2, ldC;
   hipStream_t stream = nullptr;
   bool own_stream = true;
   std::string err;
@@ -274,14 +274,14 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
   const Layout& L = c->L;
   GemmEpi e = epi_none();
   e.out = h1;
-  e.ldo = c->ldH1;
+  e.ldo = c->ldAH1;
   e.bias = P(c, base, L.a[AB1]);
   e.act = 1;
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.a[AW1]), c->H1, B, c->H1, c->S,
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.a[AW1]), c->AH1, B, c->AH1, c->S,
                           e);
   e = epi_none();
   e.out = h2;
-  e.ldo = c->ldH2;
+  e.ldo = c->ldAH2;
   e.bias = P(c, base, L.a[AB2]);
   e.act = 1;
   e.proj = P(c, base, L.a[AW3]);
@@ -289,9 +289,9 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
   e.proj_sn = c->A;
   e.proj_sa = 1;
   e.proj_out = c->ppart;
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd_head", h1, c->ldH1, P(c, base, L.a[AW2]), c->H2, B,
-                          c->H2, c->H1, e);
-  const int NT = ceil_div(c->H2, GBN);
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd_head", h1, c->ldAH1, P(c, base, L.a[AW2]), c->AH2, B,
+                          c->AH2, c->AH1, e);
+  const int NT = ceil_div(c->AH2, GBN);
   {
     ProfScope ps(c, "actor_out", 0, 0);
     hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
@@ -312,11 +312,11 @@ static void critic_fwd(ddpg_ctx* c, const float* base, const float* s, const flo
   e.ldo = c->ldC;
   e.bias = P(c, base, L.c[CBS]);
   e.act = 1;
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.c[CWS]), c->H1, B, c->H1, c->S,
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1, c->S,
                           e);
-  e.out = cat + c->H1;
+  e.out = cat + c->CH1;
   e.bias = P(c, base, L.c[CBA]);
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", a, c->ldA, P(c, base, L.c[CWA]), c->H1, B, c->H1, c->A,
+  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1, c->A,
                           e);
   e = epi_none();
   e.bias = P(c, base, L.c[CBH]);
@@ -325,10 +325,10 @@ static void critic_fwd(ddpg_ctx* c, const float* base, const float* s, const flo
     e.post = 2;
     e.pw = P(c, base, L.c[CWO]);
     e.out = dhp_out;
-    e.ldo = c->ldH2;
+    e.ldo = c->ldCH2;
   } else {
     e.out = (mode == 0) ? h_out : nullptr;
-    e.ldo = c->ldH2;
+    e.ldo = c->ldCH2;
     e.proj = P(c, base, L.c[CWO]);
     e.proj_n = 1;
     e.proj_sn = 1;
@@ -336,7 +336,7 @@ static void critic_fwd(ddpg_ctx* c, const float* base, const float* s, const flo
     e.proj_out = c->qpart;
   }
   gemm_launch<L_RK, L_KR>(c, mode == 2 ? "gemm_fwd" : "gemm_fwd_head", cat, c->ldC,
-                          P(c, base, L.c[CWH]), c->H2, B, c->H2, 2 * c->H1, e);
+                          P(c, base, L.c[CWH]), c->CH2, B, c->CH2, 2 * c->CH1, e);
 }
 
 // dQ/da of the (already updated) online critic at (s, a): networks.py:143.
@@ -347,20 +347,20 @@ static void critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int 
   critic_fwd(c, c->theta, s, a, B, c->cat2, nullptr, 2, c->dhp2);
   GemmEpi e = epi_none();
   e.post = 1;
-  e.aux = c->cat2 + c->H1;
+  e.aux = c->cat2 + c->CH1;
   e.ldaux = c->ldC;
   e.proj = P(c, c->theta, L.c[CWA]);
   e.proj_n = c->A;
   e.proj_sn = 1;
-  e.proj_sa = c->H1;
+  e.proj_sa = c->CH1;
   e.proj_out = c->ppart;
   // B operand = Wh[H1:2H1, :]^T  (NK: element (k=j, n=i) at Wh[(H1+i)*H2 + j])
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp2, c->ldH2,
-                          P(c, c->theta, L.c[CWH]) + (size_t)c->H1 * c->H2, c->H2, B, c->H1, c->H2,
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp2, c->ldCH2,
+                          P(c, c->theta, L.c[CWH]) + (size_t)c->CH1 * c->CH2, c->CH2, B, c->CH1, c->CH2,
                           e);
   ProfScope ps(c, "action_grad", 0, 0);
   hipLaunchKernelGGL(action_grad_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
-                     c->ppart, ceil_div(c->H1, GBN), B, c->A, B, o, c->ldA,
+                     c->ppart, ceil_div(c->CH1, GBN), B, c->A, B, o, c->ldA,
                      c->cfg.action_scale, da, dz3);
   HIP_TRY(hipGetLastError());
 }
@@ -421,28 +421,28 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
   {
     ProfScope ps(c, "critic_loss", 0, 0);
     hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->stream, c->qpart,
-                       ceil_div(c->H2, GBN), B, P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q,
+                       ceil_div(c->CH2, GBN), B, P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q,
                        c->dq, c->dstats, c->dacc);
     HIP_TRY(hipGetLastError());
   }
   const int nchunk = ceil_div(B, kHeadRows);
   float* part_dWo = c->headpart;
-  float* part_dbh = c->headpart + (size_t)nchunk * c->H2;
-  float* part_dbo = part_dbh + (size_t)nchunk * c->H2;
+  float* part_dbh = c->headpart + (size_t)nchunk * c->CH2;
+  float* part_dbo = part_dbh + (size_t)nchunk * c->CH2;
   {
-    ProfScope ps(c, "critic_head_bwd", 0, (double)B * c->H2 * 8.0);
-    hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->H2, 256), nchunk), dim3(256), 0,
-                       c->stream, c->h, c->ldH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->H2,
-                       kHeadRows, c->dhp, c->ldH2, part_dWo, part_dbh, part_dbo);
+    ProfScope ps(c, "critic_head_bwd", 0, (double)B * c->CH2 * 8.0);
+    hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->CH2, 256), nchunk), dim3(256), 0,
+                       c->stream, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->CH2,
+                       kHeadRows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo);
     HIP_TRY(hipGetLastError());
   }
   // dWh = cat^T . dh_pre   (split-K slabs)
-  const int sWh = std::min(c->split_cap_Wh, wgrad_splits(2 * c->H1, c->H2, B));
+  const int sWh = std::min(c->split_cap_Wh, wgrad_splits(2 * c->CH1, c->CH2, B));
   GemmEpi e = epi_none();
   e.out = c->slab_Wh;
-  e.ldo = c->H2;
-  e.out_split_stride = (long long)2 * c->H1 * c->H2;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->cat, c->ldC, c->dhp, c->ldH2, 2 * c->H1, c->H2, B,
+  e.ldo = c->CH2;
+  e.out_split_stride = (long long)2 * c->CH1 * c->CH2;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1, c->CH2, B,
                           e, sWh);
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
   const int mt = ceil_div(B, GBM);
@@ -453,20 +453,20 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
   e.out = c->dcat;
   e.ldo = c->ldC;
   e.colsum = c->colpart;
-  e.ld_colsum = 2 * c->H1;
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp, c->ldH2, P(c, c->theta, L.c[CWH]), c->H2, B,
-                          2 * c->H1, c->H2, e);
+  e.ld_colsum = 2 * c->CH1;
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]), c->CH2, B,
+                          2 * c->CH1, c->CH2, e);
   // dWs = s^T . dcs ; dWa = a^T . dca
-  const int sWs = std::min(c->split_cap_Ws, wgrad_splits(c->S, c->H1, B));
+  const int sWs = std::min(c->split_cap_Ws, wgrad_splits(c->S, c->CH1, B));
   e = epi_none();
   e.out = c->slab_Ws;
-  e.ldo = c->H1;
-  e.out_split_stride = (long long)c->S * c->H1;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->H1, B, e, sWs);
-  const int sWa = std::min(c->split_cap_Wa, wgrad_splits(c->A, c->H1, B));
+  e.ldo = c->CH1;
+  e.out_split_stride = (long long)c->S * c->CH1;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, e, sWs);
+  const int sWa = std::min(c->split_cap_Wa, wgrad_splits(c->A, c->CH1, B));
   e.out = c->slab_Wa;
-  e.out_split_stride = (long long)c->A * c->H1;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->a, c->ldA, c->dcat + c->H1, c->ldC, c->A, c->H1, B,
+  e.out_split_stride = (long long)c->A * c->CH1;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A, c->CH1, B,
                           e, sWa);
   // gather every critic gradient into the flat grad buffer
   float* G = c->grad;
@@ -478,16 +478,16 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
     int kps = rup(std::max(1, ceil_div(K, s)), GBK);
     return std::max(1, ceil_div(K, kps));
   };
-  add_seg(tab, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->H1, gsplits(sWs, B), c->S,
-          c->H1, c->H1);
-  add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->H1, mt, 1, c->H1, 0);
-  add_seg(tab, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->H1, gsplits(sWa, B), c->A,
-          c->H1, c->H1);
-  add_seg(tab, c->colpart + c->H1, G + L.c[CBA].off, 2 * c->H1, mt, 1, c->H1, 0);
-  add_seg(tab, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->H1 * c->H2, gsplits(sWh, B),
-          2 * c->H1, c->H2, c->H2);
-  add_seg(tab, part_dbh, G + L.c[CBH].off, c->H2, nchunk, 1, c->H2, 0);
-  add_seg(tab, part_dWo, G + L.c[CWO].off, c->H2, nchunk, 1, c->H2, 0);
+  add_seg(tab, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1, gsplits(sWs, B), c->S,
+          c->CH1, c->CH1);
+  add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, 1, c->CH1, 0);
+  add_seg(tab, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1, gsplits(sWa, B), c->A,
+          c->CH1, c->CH1);
+  add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, 1, c->CH1, 0);
+  add_seg(tab, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->CH1 * c->CH2, gsplits(sWh, B),
+          2 * c->CH1, c->CH2, c->CH2);
+  add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, 1, c->CH2, 0);
+  add_seg(tab, part_dWo, G + L.c[CWO].off, c->CH2, nchunk, 1, c->CH2, 0);
   add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1, 1, 0);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.critic_begin, L.critic_end - L.critic_begin);
@@ -501,50 +501,50 @@ static void actor_train_dev(ddpg_ctx* c, int B) {
   float* G = c->grad;
   const int mt = ceil_div(B, GBM);
   // dW3 = h2^T . dz3
-  const int sW3 = std::min(c->split_cap_W3, wgrad_splits(c->H2, c->A, B));
+  const int sW3 = std::min(c->split_cap_W3, wgrad_splits(c->AH2, c->A, B));
   GemmEpi e = epi_none();
   e.out = c->slab_W3;
   e.ldo = c->A;
-  e.out_split_stride = (long long)c->H2 * c->A;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h2, c->ldH2, c->dz3, c->ldA, c->H2, c->A, B, e, sW3);
+  e.out_split_stride = (long long)c->AH2 * c->A;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, e, sW3);
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
   e = epi_none();
   e.post = 1;
   e.aux = c->h2;
-  e.ldaux = c->ldH2;
+  e.ldaux = c->ldAH2;
   e.out = c->dz2;
-  e.ldo = c->ldH2;
+  e.ldo = c->ldAH2;
   e.colsum = c->colpart;
-  e.ld_colsum = c->H2;
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A, B, c->H2,
+  e.ld_colsum = c->AH2;
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A, B, c->AH2,
                           c->A, e);
   // dW2 = h1^T . dz2
-  const int sW2 = std::min(c->split_cap_W2, wgrad_splits(c->H1, c->H2, B));
+  const int sW2 = std::min(c->split_cap_W2, wgrad_splits(c->AH1, c->AH2, B));
   e = epi_none();
   e.out = c->slab_W2;
-  e.ldo = c->H2;
-  e.out_split_stride = (long long)c->H1 * c->H2;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h1, c->ldH1, c->dz2, c->ldH2, c->H1, c->H2, B, e,
+  e.ldo = c->AH2;
+  e.out_split_stride = (long long)c->AH1 * c->AH2;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1, c->AH2, B, e,
                           sW2);
   // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
-  float* colpart1 = c->colpart + (size_t)mt * c->H2;
+  float* colpart1 = c->colpart + (size_t)mt * c->AH2;
   e = epi_none();
   e.post = 1;
   e.aux = c->h1;
-  e.ldaux = c->ldH1;
+  e.ldaux = c->ldAH1;
   e.out = c->dz1;
-  e.ldo = c->ldH1;
+  e.ldo = c->ldAH1;
   e.colsum = colpart1;
-  e.ld_colsum = c->H1;
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz2, c->ldH2, P(c, c->theta, L.a[AW2]), c->H2, B,
-                          c->H1, c->H2, e);
+  e.ld_colsum = c->AH1;
+  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz2, c->ldAH2, P(c, c->theta, L.a[AW2]), c->AH2, B,
+                          c->AH1, c->AH2, e);
   // dW1 = s^T . dz1
-  const int sW1 = std::min(c->split_cap_W1, wgrad_splits(c->S, c->H1, B));
+  const int sW1 = std::min(c->split_cap_W1, wgrad_splits(c->S, c->AH1, B));
   e = epi_none();
   e.out = c->slab_W1;
-  e.ldo = c->H1;
-  e.out_split_stride = (long long)c->S * c->H1;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dz1, c->ldH1, c->S, c->H1, B, e, sW1);
+  e.ldo = c->AH1;
+  e.out_split_stride = (long long)c->S * c->AH1;
+  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1, B, e, sW1);
 
   auto gsplits = [&](int s, int K) {
     int kps = rup(std::max(1, ceil_div(K, s)), GBK);
@@ -552,13 +552,13 @@ static void actor_train_dev(ddpg_ctx* c, int B) {
   };
   ReduceTable tab;
   tab.nseg = 0;
-  add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->H1, gsplits(sW1, B), c->S, c->H1,
-          c->H1);
-  add_seg(tab, colpart1, G + L.a[AB1].off, c->H1, mt, 1, c->H1, 0);
-  add_seg(tab, c->slab_W2, G + L.a[AW2].off, (long long)c->H1 * c->H2, gsplits(sW2, B), c->H1,
-          c->H2, c->H2);
-  add_seg(tab, c->colpart, G + L.a[AB2].off, c->H2, mt, 1, c->H2, 0);
-  add_seg(tab, c->slab_W3, G + L.a[AW3].off, (long long)c->H2 * c->A, gsplits(sW3, B), c->H2,
+  add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1, gsplits(sW1, B), c->S, c->AH1,
+          c->AH1);
+  add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, mt, 1, c->AH1, 0);
+  add_seg(tab, c->slab_W2, G + L.a[AW2].off, (long long)c->AH1 * c->AH2, gsplits(sW2, B), c->AH1,
+          c->AH2, c->AH2);
+  add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt, 1, c->AH2, 0);
+  add_seg(tab, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A, gsplits(sW3, B), c->AH2,
           c->A, c->A);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.actor_begin, L.actor_end - L.actor_begin);
@@ -594,7 +594,7 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   {
     ProfScope ps(c, "td_target", 0, 0);
     hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
-                       ceil_div(c->H2, GBN), B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t,
+                       ceil_div(c->CH2, GBN), B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t,
                        c->cfg.gamma, c->y);
     HIP_TRY(hipGetLastError());
   }
@@ -699,7 +699,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
   memset(c->slot_ev, 0, sizeof c->slot_ev);
   int rc = guard(c, [&] {
     const ddpg_cfg& k = *cfg;
-    if (k.state_dim <= 0 || k.action_dim <= 0 || k.h1 <= 0 || k.h2 <= 0 || k.batch_max <= 0)
+    if (k.state_dim <= 0 || k.action_dim <= 0 || k.h1 <= 0 || k.h2 <= 0 || k.batch_max <= 0 ||
+        k.critic_h1 < 0 || k.critic_h2 < 0)
       throw einval("dims must be positive (S=%d A=%d H1=%d H2=%d Bmax=%d)", k.state_dim,
                    k.action_dim, k.h1, k.h2, k.batch_max);
     if (k.action_dim > PROJ_MAX) throw einval("action_dim %d > %d", k.action_dim, PROJ_MAX);
@@ -707,17 +708,20 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     c->cfg = k;
     c->S = k.state_dim;
     c->A = k.action_dim;
-    c->H1 = k.h1;
-    c->H2 = k.h2;
+    c->AH1 = k.h1;
+    c->AH2 = k.h2;
+    c->CH1 = k.critic_h1 > 0 ? k.critic_h1 : k.h1;
+    c->CH2 = k.critic_h2 > 0 ? k.critic_h2 : k.h2;
     c->Bmax = k.batch_max;
     c->world = std::max(1, k.world);
     c->rank = k.rank;
     c->ldS = rup(c->S, 4);
     c->ldA = rup(c->A, 4);
-    c->ldH1 = rup(c->H1, 4);
-    c->ldH2 = rup(c->H2, 4);
-    c->ldC = rup(2 * c->H1, 4);
-    c->L.build(c->S, c->A, c->H1, c->H2);
+    c->ldAH1 = rup(c->AH1, 4);
+    c->ldAH2 = rup(c->AH2, 4);
+    c->ldCH2 = rup(c->CH2, 4);
+    c->ldC = rup(2 * c->CH1, 4);
+    c->L.build(c->S, c->A, c->AH1, c->AH2, c->CH1, c->CH2);
     HIP_TRY(hipSetDevice(k.device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     const size_t PT = c->L.total;
@@ -740,15 +744,16 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
 
     // activation workspace
     const size_t B = (size_t)c->Bmax;
-    const int NT2 = ceil_div(c->H2, GBN), NT1 = ceil_div(c->H1, GBN);
+    const int NTP = std::max(ceil_div(c->AH2, GBN), ceil_div(c->CH1, GBN));
+    const int NTQ = ceil_div(c->CH2, GBN);
     const int mt = ceil_div(c->Bmax, GBM);
     const int nchunk = ceil_div(c->Bmax, kHeadRows);
-    c->split_cap_W1 = wgrad_splits(c->S, c->H1, c->Bmax);
-    c->split_cap_W2 = wgrad_splits(c->H1, c->H2, c->Bmax);
-    c->split_cap_W3 = wgrad_splits(c->H2, c->A, c->Bmax);
-    c->split_cap_Ws = wgrad_splits(c->S, c->H1, c->Bmax);
-    c->split_cap_Wa = wgrad_splits(c->A, c->H1, c->Bmax);
-    c->split_cap_Wh = wgrad_splits(2 * c->H1, c->H2, c->Bmax);
+    c->split_cap_W1 = wgrad_splits(c->S, c->AH1, c->Bmax);
+    c->split_cap_W2 = wgrad_splits(c->AH1, c->AH2, c->Bmax);
+    c->split_cap_W3 = wgrad_splits(c->AH2, c->A, c->Bmax);
+    c->split_cap_Ws = wgrad_splits(c->S, c->CH1, c->Bmax);
+    c->split_cap_Wa = wgrad_splits(c->A, c->CH1, c->Bmax);
+    c->split_cap_Wh = wgrad_splits(2 * c->CH1, c->CH2, c->Bmax);
     struct Req {
       float** p;
       size_t n;
@@ -756,23 +761,23 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     std::vector<Req> req = {
         {&c->s, B * c->ldS},   {&c->s2, B * c->ldS},   {&c->a, B * c->ldA},
         {&c->r, B},            {&c->t, B},             {&c->y, B},
-        {&c->q, B},            {&c->dq, B},            {&c->th1, B * c->ldH1},
+        {&c->q, B},            {&c->dq, B},            {&c->th1, B * c->ldAH1},
         {&c->tcat, B * c->ldC}, {&c->ta2, B * c->ldA}, {&c->cat, B * c->ldC},
-        {&c->h, B * c->ldH2},  {&c->dhp, B * c->ldH2}, {&c->dcat, B * c->ldC},
-        {&c->h1, B * c->ldH1}, {&c->h2, B * c->ldH2},  {&c->o, B * c->ldA},
-        {&c->mu, B * c->ldA},  {&c->cat2, B * c->ldC}, {&c->dhp2, B * c->ldH2},
-        {&c->da, B * c->ldA},  {&c->dz3, B * c->ldA},  {&c->dz2, B * c->ldH2},
-        {&c->dz1, B * c->ldH1}, {&c->dain, B * c->A},
-        {&c->ppart, (size_t)std::max(NT1, NT2) * B * PROJ_MAX},
-        {&c->qpart, (size_t)NT2 * B},
-        {&c->colpart, (size_t)mt * (c->H2 + std::max(2 * c->H1, c->H1))},
-        {&c->headpart, (size_t)nchunk * (2 * c->H2 + 1)},
-        {&c->slab_W1, (size_t)c->split_cap_W1 * c->S * c->H1},
-        {&c->slab_W2, (size_t)c->split_cap_W2 * c->H1 * c->H2},
-        {&c->slab_W3, (size_t)c->split_cap_W3 * c->H2 * c->A},
-        {&c->slab_Ws, (size_t)c->split_cap_Ws * c->S * c->H1},
-        {&c->slab_Wa, (size_t)c->split_cap_Wa * c->A * c->H1},
-        {&c->slab_Wh, (size_t)c->split_cap_Wh * 2 * c->H1 * c->H2},
+        {&c->h, B * c->ldCH2},  {&c->dhp, B * c->ldCH2}, {&c->dcat, B * c->ldC},
+        {&c->h1, B * c->ldAH1}, {&c->h2, B * c->ldAH2},  {&c->o, B * c->ldA},
+        {&c->mu, B * c->ldA},  {&c->cat2, B * c->ldC}, {&c->dhp2, B * c->ldCH2},
+        {&c->da, B * c->ldA},  {&c->dz3, B * c->ldA},  {&c->dz2, B * c->ldAH2},
+        {&c->dz1, B * c->ldAH1}, {&c->dain, B * c->A},
+        {&c->ppart, (size_t)NTP * B * PROJ_MAX},
+        {&c->qpart, (size_t)NTQ * B},
+        {&c->colpart, (size_t)mt * std::max(2 * c->CH1, c->AH2 + c->AH1)},
+        {&c->headpart, (size_t)nchunk * (2 * c->CH2 + 1)},
+        {&c->slab_W1, (size_t)c->split_cap_W1 * c->S * c->AH1},
+        {&c->slab_W2, (size_t)c->split_cap_W2 * c->AH1 * c->AH2},
+        {&c->slab_W3, (size_t)c->split_cap_W3 * c->AH2 * c->A},
+        {&c->slab_Ws, (size_t)c->split_cap_Ws * c->S * c->CH1},
+        {&c->slab_Wa, (size_t)c->split_cap_Wa * c->A * c->CH1},
+        {&c->slab_Wh, (size_t)c->split_cap_Wh * 2 * c->CH1 * c->CH2},
     };
     size_t tot = 0;
     for (auto& r : req) tot += (r.n + 63) / 64 * 64;
@@ -949,7 +954,7 @@ int ddpg_critic_forward(ddpg_ctx* c, int target, const float* s, const float* a,
     const float* base = target ? c->target : c->theta;
     critic_fwd(c, base, c->s, c->a, B, c->cat, nullptr, 1, nullptr);
     hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
-                       ceil_div(c->H2, GBN), B, P(c, base, c->L.c[CBO]), c->q, 0, nullptr,
+                       ceil_div(c->CH2, GBN), B, P(c, base, c->L.c[CBO]), c->q, 0, nullptr,
                        nullptr, 0.f, nullptr);
     HIP_TRY(hipGetLastError());
     download_rows(c, q_out, c->q, 1, B, 1);

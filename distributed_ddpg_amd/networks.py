@@ -76,8 +76,7 @@ class Session:
         cfg = _lib.Cfg()
         cfg.state_dim, cfg.action_dim = a.s_dim, a.a_dim
         cfg.h1, cfg.h2 = a.h1, a.h2
-        if (c.h1, c.h2) != (a.h1, a.h2):
-            raise ValueError("this build shares hidden widths between actor and critic")
+        cfg.critic_h1, cfg.critic_h2 = c.h1, c.h2
         cfg.batch_max = self.batch_max
         cfg.actor_lr, cfg.critic_lr = a.learning_rate, c.learning_rate
         if a.tau != c.tau:
@@ -107,8 +106,8 @@ class Session:
         (networks.py:30,122 build targets with their own initialisers)."""
         from .init import init_network_params
         a, c = self.actor, self.critic
-        online = init_network_params(a.s_dim, a.a_dim, a.h1, a.h2, seed)
-        target = init_network_params(a.s_dim, a.a_dim, a.h1, a.h2, seed + 1)
+        online = init_network_params(a.s_dim, a.a_dim, a.h1, a.h2, seed, c.h1, c.h2)
+        target = init_network_params(a.s_dim, a.a_dim, a.h1, a.h2, seed + 1, c.h1, c.h2)
         self.set_params(_lib.ACTOR, online[0])
         self.set_params(_lib.CRITIC, online[1])
         self.set_params(_lib.ACTOR_TARGET, target[0])

@@ -63,7 +63,7 @@ enum ddpg_which {
 typedef struct ddpg_cfg {
   int state_dim;      /* S */
   int action_dim;     /* A */
-  int h1, h2;         /* hidden widths (reference: 128 / 200, networks.py:54-55,151-156) */
+  int h1, h2;         /* actor hidden widths (reference: 128 / 200, networks.py:54-55) */
   int batch_max;      /* max rows per call (per rank) */
   float actor_lr;     /* parameters.py:15  (1e-4) */
   float critic_lr;    /* parameters.py:14  (1e-3) */
@@ -74,6 +74,8 @@ typedef struct ddpg_cfg {
   int dtype;          /* ddpg_dtype: GEMM operand precision (fp32 master state always) */
   int device;         /* HIP device ordinal */
   int rank, world;    /* data-parallel position; world==1 -> no collectives */
+  int critic_h1, critic_h2; /* critic widths (networks.py:151-156); 0 = same as actor.
+                             * The reference's MountainCar checkpoint uses 48/64 vs 48/128. */
 } ddpg_cfg;
 
 typedef struct ddpg_ctx ddpg_ctx;

@@ -247,8 +247,9 @@ class Learner:
     actor forward inside actor.train as TF does (cost only; same numbers)."""
 
     def __init__(self, S, A, H1, H2, scale, actor_lr=1e-4, critic_lr=1e-3, tau=1e-3,
-                 gamma=0.99, dtype=np.float64, params=None, init_blend=True):
+                 gamma=0.99, dtype=np.float64, params=None, init_blend=True, CH1=None, CH2=None):
         self.S, self.A, self.H1, self.H2 = S, A, H1, H2
+        CH1, CH2 = CH1 or H1, CH2 or H2
         self.scale, self.tau, self.gamma = scale, tau, gamma
         self.dtype = np.dtype(dtype)
         if params is None:
@@ -257,7 +258,7 @@ class Learner:
         self.actor, self.actor_t = cv(params["actor"]), cv(params["actor_t"])
         self.critic, self.critic_t = cv(params["critic"]), cv(params["critic_t"])
         self.actor_opt = TFAdam(actor_shapes(S, A, H1, H2), actor_lr, self.dtype)
-        self.critic_opt = TFAdam(critic_shapes(S, A, H1, H2), critic_lr, self.dtype)
+        self.critic_opt = TFAdam(critic_shapes(S, A, CH1, CH2), critic_lr, self.dtype)
         if init_blend:  # ddpg.py:224-229
             soft_update(self.actor, self.actor_t, tau)
             soft_update(self.critic, self.critic_t, tau)

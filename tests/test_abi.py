@@ -47,7 +47,7 @@ def test_abi_version_and_errors_without_gpu():
 
 
 def test_cfg_struct_layout():
-    """ddpg_cfg is 17 x 4-byte fields, no padding (matches the header)."""
+    """ddpg_cfg is 19 x 4-byte fields, no padding (matches the header)."""
     from distributed_ddpg_amd import _lib
-    assert _lib.ctypes.sizeof(_lib.Cfg) == 17 * 4
+    assert _lib.ctypes.sizeof(_lib.Cfg) == 19 * 4
     assert _lib.ctypes.sizeof(_lib.Stats) == 8

@@ -7,6 +7,14 @@ over each tensor:
   soft update                              bit-exact (same fp32 ops as TF)
   replay indices / gathered rows           bit-exact
 The oracle runs in float64 on the same fp32 inputs and weights.
+
+Multi-step fused runs: Adam normalises every gradient element to ~lr, so
+elements whose gradient is a near-cancelling fp32 sum carry fp32 rounding
+straight into the parameter.  A TF-semantics fp32 restatement (the oracle in
+float32, i.e. what the reference's TF 1.3 CPU path computes) drifts from fp64
+by up to ~7e-5 on such tensors after 4 steps.  The multi-step bar is therefore
+  max-rel  <= max(1e-4, 3 x the fp32 restatement's own max-rel drift), and
+  norm-rel (||x - ref||_2 / ||ref||_2) <= 1e-5.
 """
 import os
 
@@ -44,12 +52,19 @@ def dd():
 
 
 CONFIGS = {
-    # name: S, A, H1, H2, scale, B, source
+    # name: S, A, H1, H2, scale, B, source  (critic widths in CRITIC_W when they differ)
     "ip": (4, 1, 128, 200, 3.0, 64, "ip_model1410"),
     "mc": (2, 1, 48, 64, 1.0, 64, "mc_model120"),
     "odd": (5, 3, 40, 72, 2.0, 37, None),
     "wide": (64, 16, 1024, 1024, 1.0, 256, None),
 }
+# the MountainCar checkpoint's critic is 48/128 while its actor is 48/64
+CRITIC_W = {"mc": (48, 128)}
+
+
+def cw(name):
+    S, A, H1, H2 = CONFIGS[name][:4]
+    return CRITIC_W.get(name, (H1, H2))
 
 
 def _params(O, name):
@@ -63,6 +78,7 @@ def _params(O, name):
         return p, z
     a, c = O.init_params(S, A, H1, H2, seed=11)
     at, ct = O.init_params(S, A, H1, H2, seed=12)
+    assert name not in CRITIC_W
     # larger-than-init weights so every branch (elu < 0, tanh saturation) is exercised
     rng = np.random.default_rng(3)
     for d in (a, c, at, ct):
@@ -77,7 +93,9 @@ def _session(dd, O, name, p, batch_max=4096):
     from distributed_ddpg_amd import _lib
     dd.reset_default_graph()
     actor = dd.ActorNetwork(S, A, scale, 1e-4, 1e-3, None, h1=H1, h2=H2)
-    critic = dd.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), None, h1=H1, h2=H2)
+    CH1, CH2 = cw(name)
+    critic = dd.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), None, h1=CH1,
+                              h2=CH2)
     sess = dd.Session(batch_max=batch_max)
     actor.set_session(sess)
     critic.set_session(sess)
@@ -95,6 +113,19 @@ def _batch(name, seed=0, B=None):
     s = rng.standard_normal((B, S)).astype(np.float32)
     a = (rng.uniform(-1, 1, (B, A)) * scale).astype(np.float32)
     return s, a, rng
+
+
+def normrel(x, ref):
+    x = np.asarray(x, np.float64).ravel()
+    ref = np.asarray(ref, np.float64).ravel()
+    return float(np.linalg.norm(x - ref) / max(np.linalg.norm(ref), 1e-30))
+
+
+def assert_steps_close(v, ref64, ref32, what):
+    floor = rel(ref32.reshape(v.shape), ref64.reshape(v.shape))
+    err = rel(v, ref64.reshape(v.shape))
+    assert err <= max(GRAD_TOL, 3 * floor), (what, err, floor)
+    assert normrel(v, ref64) <= 1e-5, (what, normrel(v, ref64))
 
 
 def f64(d):
@@ -132,7 +163,7 @@ def test_train_methods_parity(dd, O, name):
     p, _ = _params(O, name)
     sess, actor, critic = _session(dd, O, name, p)
     L = O.Learner(S, A, H1, H2, scale, actor_lr=1e-4, critic_lr=1e-3, tau=1e-3,
-                  dtype=np.float64, params=p, init_blend=False)
+                  dtype=np.float64, params=p, init_blend=False, CH1=cw(name)[0], CH2=cw(name)[1])
     for it in range(3):
         s, a, rng = _batch(name, seed=10 + it)
         y = rng.standard_normal((B, 1)).astype(np.float32)
@@ -203,7 +234,8 @@ def test_mc_checkpoint_adam_resume(dd, O):
     sess.set_params(_lib.CRITIC_ADAM_V, slots(O.CKPT_CRITIC, "/Adam_1"))
     sess.set_adam_powers(0, float(z["beta1_power"]), float(z["beta2_power"]))
     sess.set_adam_powers(1, float(z["beta1_power_1"]), float(z["beta2_power_1"]))
-    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False,
+                  CH1=cw("mc")[0], CH2=cw("mc")[1])
     for net, names in ((L.actor_opt, O.CKPT_ACTOR), (L.critic_opt, O.CKPT_CRITIC)):
         keys = O.ACTOR_KEYS if names is O.CKPT_ACTOR else O.CRITIC_KEYS
         for k, n in zip(keys, names):
@@ -283,20 +315,22 @@ def test_fused_learner_step_parity(dd, O, name):
     rows = _fill(rb, S, A, 3000, scale, seed=2)
     fl = FusedLearner(sess, rb, B)
     L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    L32 = O.Learner(S, A, H1, H2, scale, dtype=np.float32, params=p, init_blend=False)
     ref_rng = random.Random(1234)  # the reference's global RNG after random.seed(1234)
     for it in range(4):
         idx = np.array(ref_rng.sample(range(3000), B))
         qmax, loss = fl.step(stats=True)
         s, a, r, t, s2 = (x[idx] for x in rows)
         out = L.step(s, a, r, t, s2)
+        L32.step(s, a, r, t, s2)
         assert abs(qmax - float(np.max(out["q"]))) <= FWD_TOL * max(1.0, abs(np.max(out["q"]))) * 10
         assert abs(loss - float(out["loss"])) <= GRAD_TOL * abs(float(out["loss"]))
-    for which, ref, keys in ((_lib.ACTOR, L.actor, O.ACTOR_KEYS),
-                             (_lib.CRITIC, L.critic, O.CRITIC_KEYS),
-                             (_lib.ACTOR_TARGET, L.actor_t, O.ACTOR_KEYS),
-                             (_lib.CRITIC_TARGET, L.critic_t, O.CRITIC_KEYS)):
+    for which, net, keys in ((_lib.ACTOR, "actor", O.ACTOR_KEYS),
+                             (_lib.CRITIC, "critic", O.CRITIC_KEYS),
+                             (_lib.ACTOR_TARGET, "actor_t", O.ACTOR_KEYS),
+                             (_lib.CRITIC_TARGET, "critic_t", O.CRITIC_KEYS)):
         for k, v in zip(keys, sess.get_params(which)):
-            assert rel(v, ref[k].reshape(v.shape)) < GRAD_TOL, (which, k)
+            assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (net, k))
     q_sum, l_sum, n = fl.read_stats()
     assert n == 4
     sess.close()
