@@ -1,0 +1,272 @@
+"""Benchmark: DDPG actor+critic learner updates/s on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
+
+One "step" = one whole learner update (ddpg.py:86-113) as ddpg_learner_step:
+host MT19937 draw of the batch from a replay ring filled to 1e6 synthetic
+transitions, device gather, target/critic/actor forward and
+backward, both Adam updates, both soft updates.  Inputs are resident in HBM
+before the timed region.  N>1: one process per GPU (torchrun), synchronous
+data parallelism, RCCL all-reduce of the critic then actor gradients, weak
+scaling (per-GPU batch fixed), value = batch-sized updates processed by all
+ranks / max-over-ranks time.
+
+Rank 0 prints ONE JSON line with the contract fields plus
+  roofline      dominant kernel (HIP-event timed in-process) vs fp32 MFMA peak
+  cpu_baseline  the oracle's TF-op-sequence restatement (numpy fp32) on host cores
+  small_batch   the InvertedPendulum B=64 latency-bound configuration (N=1 only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix) 157.3 TF spec
+PEAK_HBM_GBS = 8000.0           # 8 TB/s spec
+
+CONFIGS = {
+    # name: (S, A, H1, H2, B per GPU, action_scale, label)
+    "c3": (64, 16, 1024, 1024, 4096, 1.0,
+           "C3 synthetic S=64 A=16 actor/critic 1024/1024, batch 4096/GPU, fp32"),
+    "c2": (4, 1, 128, 200, 64, 3.0,
+           "C2 InvertedPendulum-shaped S=4 A=1 128/200, batch 64, fp32"),
+    "c5": (376, 17, 2048, 2048, 4096, 1.0,
+           "C5 Humanoid-shaped S=376 A=17 2048/2048, batch 4096/GPU, fp32"),
+}
+REPLAY_ROWS = 1_000_000
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234):
+    from distributed_ddpg_amd import networks as nets
+    from distributed_ddpg_amd.learner import FusedLearner, fill_synthetic, init_comm
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, B, scale, _ = CONFIGS[cfg_name]
+    nets.reset_default_graph()
+    actor = nets.ActorNetwork(S, A, scale, 1e-4, 1e-3, None, h1=H1, h2=H2)
+    critic = nets.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), None, h1=H1,
+                                h2=H2)
+    sess = nets.Session(device=device, batch_max=B, rank=rank, world=world)
+    actor.set_session(sess)
+    critic.set_session(sess)
+    sess.run(nets.global_variables_initializer(seed=seed))   # same init on every rank
+    actor.update_target_network()                            # ddpg.py:228-229
+    critic.update_target_network()
+    init_comm(sess, rank, world)
+    rb = ReplayBuffer(replay_rows, seed, device=device)
+    t0 = time.time()
+    fill_synthetic(rb, S, A, replay_rows, scale=scale, seed=seed)   # identical on every rank
+    log("[bench] rank %d replay filled with %d rows in %.1fs" % (rank, replay_rows,
+                                                                 time.time() - t0))
+    return sess, rb, FusedLearner(sess, rb, B * world)
+
+
+def timed(fl, sess, steps, warmup, world):
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        fl.step()
+    sess.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    sess.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fl.step()
+    sess.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = t1 - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def kernel_profile(fl, sess, steps):
+    from distributed_ddpg_amd.learner import Profile
+    prof = Profile(sess)
+    prof.enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fl.step()
+    sess.sync()
+    wall = time.perf_counter() - t0
+    rows = prof.read()
+    prof.enable(False)
+    return rows, wall
+
+
+def summarize_profile(rows, steps):
+    by_kernel = {}
+    for key, r in rows.items():
+        sym = key.split("|")[0]
+        k = by_kernel.setdefault(sym, {"ms": 0.0, "launches": 0, "flops": 0.0, "bytes": 0.0})
+        for f in ("ms", "launches", "flops", "bytes"):
+            k[f] += r[f]
+    gpu_ms = sum(r["ms"] for r in rows.values()) / steps
+    gemm_ms = sum(r["ms"] for k, r in by_kernel.items() if k.startswith("gemm")) / steps
+    gemm_flops = sum(r["flops"] for k, r in by_kernel.items() if k.startswith("gemm")) / steps
+    dom = max(by_kernel.items(), key=lambda kv: kv[1]["ms"])
+    return by_kernel, dom, gpu_ms, gemm_ms, gemm_flops
+
+
+def cpu_baseline(cfg_name, budget_s=12.0):
+    """Oracle (numpy fp32, TF op sequence incl. actor-forward recompute) on
+    the host cores; a bounded sample of learner steps at the same config."""
+    from oracle import ddpg_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()
+                       if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = 1
+    S, A, H1, H2, B, scale, _ = CONFIGS[cfg_name]
+    a, c = O.init_params(S, A, H1, H2, seed=1)
+    at, ct = O.init_params(S, A, H1, H2, seed=2)
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float32,
+                  params={"actor": a, "actor_t": at, "critic": c, "critic_t": ct})
+    rng = np.random.default_rng(0)
+    pool = 20000
+    rows = (rng.standard_normal((pool, S), dtype=np.float32),
+            (rng.uniform(-1, 1, (pool, A)) * scale).astype(np.float32),
+            rng.standard_normal(pool, dtype=np.float32), rng.random(pool) < 0.01,
+            rng.standard_normal((pool, S), dtype=np.float32))
+    import random
+    smp = random.Random(1234)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        idx = np.array(smp.sample(range(pool), B))
+        L.step(*(x[idx] for x in rows))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": n / el, "unit": "updates/s", "cores": int(threads), "kind": "port",
+            "sample": "%d learner steps of %s (numpy fp32 oracle, TF op order incl. actor "
+                      "forward recompute; sampler = CPython random.sample) in %.1fs on %s"
+                      % (n, cfg_name.upper(), el, cpu)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--replay", type=int, default=REPLAY_ROWS)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-small", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=20)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("[bench] note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    import torch
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    cfg = args.config
+    S, A, H1, H2, B, scale, label = CONFIGS[cfg]
+    sess, rb, fl = build_learner(cfg, local, rank, world, args.replay)
+    el = timed(fl, sess, args.steps, args.warmup, world)
+    ms = 1000.0 * el / args.steps
+    value = world * args.steps / el   # batch-B updates processed by all ranks per second
+
+    rows, _ = kernel_profile(fl, sess, args.profile_steps)
+    by_kernel, (dom_name, dom), gpu_ms, gemm_ms, gemm_flops = summarize_profile(
+        rows, args.profile_steps)
+    from oracle.ddpg_oracle import flops_per_step
+    step_flops = flops_per_step(S, A, H1, H2, B)
+    dom_avg_ms = dom["ms"] / dom["launches"]
+    dom_flops = dom["flops"] / dom["launches"]
+    achieved = dom_flops / (dom_avg_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
+                "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                "avg_launch_us": round(dom_avg_ms * 1e3, 2),
+                "flop_per_launch": dom_flops, "launches_per_step":
+                    dom["launches"] / args.profile_steps}
+    out = {
+        "metric": "actor+critic updates/sec (batch %d per GPU, %d-wide MLPs)" % (B, H1),
+        "value": round(value, 3), "unit": "updates/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (replay ring of %d N(0,1)/U(-1,1)/Bernoulli(0.01) transitions; "
+                "random-init weights)" % args.replay,
+        "config": {"workload": label, "state_dim": S, "action_dim": A, "hidden": [H1, H2],
+                   "global_batch": B * world, "per_gpu_batch": B,
+                   "parallelism": "dp%d" % world},
+        "samples_per_s": round(value * B, 1),
+        "mfma_util_step": round(step_flops / (ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+        "step_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
+        "gemm_tflops": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else None,
+        "gpu_busy_ms_per_step": round(gpu_ms, 4),
+        "roofline": roofline,
+        "kernels": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
+                        "per_step": v["launches"] / args.profile_steps,
+                        "ms_per_step": round(v["ms"] / args.profile_steps, 4)}
+                    for k, v in sorted(by_kernel.items(), key=lambda kv: -kv[1]["ms"])},
+    }
+    hbm = {}
+    for key in ("adam", "soft_update", "gather"):
+        if key in by_kernel and by_kernel[key]["ms"] > 0:
+            k = by_kernel[key]
+            hbm[key] = round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1)
+    out["hbm_GBs"] = hbm
+
+    if world == 1 and rank == 0 and not args.no_small and cfg != "c2":
+        s2, rb2, fl2 = build_learner("c2", local, 0, 1, 100_000)
+        el2 = timed(fl2, s2, 500, 50, 1)
+        rows2, wall2 = kernel_profile(fl2, s2, 100)
+        busy2 = sum(r["ms"] for r in rows2.values()) / 100
+        nk2 = sum(r["launches"] for r in rows2.values()) / 100
+        out["small_batch"] = {
+            "workload": CONFIGS["c2"][6], "value": round(500 / el2, 1), "unit": "updates/s",
+            "ms_per_step": round(1000 * el2 / 500, 4),
+            "kernels_per_step": nk2, "gpu_busy_ms_per_step": round(busy2, 4),
+            "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1)}
+        s2.close()
+    if world == 1 and rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(cfg)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    sess.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -248,7 +248,11 @@ static void gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda, 
   const bool vec = (contA % 4 == 0) && (contB % 4 == 0) && (lda % 4 == 0) && (ldb % 4 == 0) &&
                    aligned16(A) && aligned16(B);
   dim3 grid(ceil_div(N, GBN), ceil_div(M, GBM), splits);
-  ProfScope ps(c, name, 2.0 * M * N * (double)K, 0.0);
+  // profile key "<kernel symbol>|<phase>": the symbol part matches rocprofv3's kernel names
+  static const char* lay[2] = {"RK", "KR"};
+  char key[96];
+  snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d>|%s", lay[AL], lay[BL], vec ? 4 : 1, name);
+  ProfScope ps(c, key, 2.0 * M * N * (double)K, 0.0);
   if (vec)
     hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, 4>), grid, dim3(GNT), 0, c->stream, g);
   else
@@ -1125,6 +1129,19 @@ int ddpg_replay_add(ddpg_replay* rb, const float* s, const float* a, const float
     HIP_TRY(hipSetDevice(rb->device));
     const size_t S = rb->S, A = rb->A;
     int done = 0;
+    if (n >= kStageRows) {  // bulk insert: straight from the caller's arrays
+      replay_flush(rb);
+      std::vector<float> rf(r, r + n), tf(n);
+      for (int i = 0; i < n; ++i) tf[i] = t[i] ? 1.f : 0.f;
+      // only the last `cap` rows can survive; skip the ones that would be overwritten
+      const int64_t skip = n > rb->cap ? n - rb->cap : 0;
+      ring_write(rb, rb->total + skip, (int)(n - skip), s + skip * S, a + skip * A, rf.data() + skip,
+                 tf.data() + skip, s2 + skip * S);
+      HIP_TRY(hipStreamSynchronize(rb->stream));
+      rb->total += n;
+      rb->count = std::min<int64_t>(rb->total, rb->cap);
+      return;
+    }
     while (done < n) {
       if (rb->st_n == 0) rb->st_first = rb->total;
       const int take = std::min(n - done, kStageRows - rb->st_n);
