@@ -119,6 +119,9 @@ struct ddpg_replay {
   int d_slots_cap = 0;
   float* d_tmp = nullptr;
   size_t d_tmp_cap = 0;
+  // recorded by learner contexts after their gather; ring writes wait on it so
+  // a queued gather never reads rows that a later add overwrote
+  hipEvent_t last_read = nullptr;
   explicit ddpg_replay(int64_t seed) : sampler(seed) {}
 };
 
@@ -158,6 +161,19 @@ struct ddpg_ctx {
   hipEvent_t slot_ev[4];
   int slot_i = 0;
   std::vector<int64_t> idx_tmp;
+
+  // hipGraph replay of the fused step: two ping-pong instances, each with its
+  // own pinned index buffer, so the host fills one while the other executes.
+  struct GraphSlot {
+    hipGraphExec_t exec = nullptr;
+    int B = -1;
+    const void* rb = nullptr;
+    bool scaler = false;
+    int* h_idx = nullptr;
+    hipEvent_t done = nullptr;
+  } gslot[2];
+  int gcur = 0;
+  bool use_graph = true;
 
   // comm
   ncclComm_t comm = nullptr;
@@ -226,10 +242,77 @@ static GemmEpi epi_none() {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Block-count target for tile selection (env DDPG_GEMM_MIN_BLOCKS overrides).
+static int g_min_blocks = 1024;
+
+struct GemmPlan {
+  int bm = 128, bn = 128, splits = 1, kps = 0;
+  int mt(int M) const { return ceil_div(M, bm); }
+  int nt(int N) const { return ceil_div(N, bn); }
+};
+
+static const int kTiles[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+
+// Largest tile (no more than one 64-row/col of padding) whose grid reaches
+// the block target; otherwise the one with the most blocks.
+static void pick_tile(int M, int N, int min_blocks, int* bm, int* bn) {
+  int best = -1, best_blocks = -1;
+  for (int t = 0; t < 4; ++t) {
+    const int tm = kTiles[t][0], tn = kTiles[t][1];
+    if (tm > 64 && M <= 64) continue;
+    if (tn > 64 && N <= 64) continue;
+    const int blocks = ceil_div(M, tm) * ceil_div(N, tn);
+    if (blocks >= min_blocks) {
+      *bm = tm;
+      *bn = tn;
+      return;
+    }
+    if (blocks > best_blocks) {
+      best_blocks = blocks;
+      best = t;
+    }
+  }
+  *bm = kTiles[best][0];
+  *bn = kTiles[best][1];
+}
+
+// Plan for a plain (splits = 1) GEMM or a split-K weight-gradient GEMM
+// (splits = 0: auto, ~512 blocks, >= 128 k per split, <= cap).
+static GemmPlan make_plan(int M, int N, int K, int splits, int cap = 64) {
+  GemmPlan p;
+  if (splits == 1) {
+    pick_tile(M, N, g_min_blocks, &p.bm, &p.bn);
+  } else {
+    p.bm = M <= 64 ? 64 : 128;
+    p.bn = N <= 64 ? 64 : 128;
+    const int tiles = ceil_div(M, p.bm) * ceil_div(N, p.bn);
+    splits = std::max(1, 512 / tiles);
+    splits = std::min(splits, std::max(1, K / 128));
+    splits = std::min(splits, cap);
+  }
+  p.kps = rup(std::max(1, ceil_div(K, splits)), GBK);
+  p.splits = std::max(1, ceil_div(K, p.kps));
+  return p;
+}
+
+template <int AL, int BL, int VEC>
+static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const GemmArgs& g) {
+  if (p.bm == 128 && p.bn == 128)
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 128, 128>), grid, dim3(GNT), 0, st, g);
+  else if (p.bm == 128)
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 128, 64>), grid, dim3(GNT), 0, st, g);
+  else if (p.bn == 128)
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 64, 128>), grid, dim3(GNT), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 64, 64>), grid, dim3(GNT), 0, st, g);
+}
+
 template <int AL, int BL>
-static void gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda, const float* B,
-                        int ldb, int M, int N, int K, const GemmEpi& e, int splits = 1) {
-  if (M <= 0 || N <= 0) return;
+static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
+                            const float* B, int ldb, int M, int N, int K, const GemmEpi& e,
+                            int splits = 1, int cap = 64) {
+  GemmPlan p = make_plan(M, N, K, splits, cap);
+  if (M <= 0 || N <= 0) return p;
   GemmArgs g;
   g.A = A;
   g.B = B;
@@ -238,41 +321,32 @@ static void gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda, 
   g.K = K;
   g.lda = lda;
   g.ldb = ldb;
-  splits = std::max(1, splits);
-  int kps = rup(std::max(1, ceil_div(K, splits)), GBK);
-  splits = std::max(1, ceil_div(K, kps));
-  g.kps = kps;
+  g.kps = p.kps;
   g.e = e;
   const int contA = (AL == L_RK) ? K : M;
   const int contB = (BL == L_RK) ? K : N;
   const bool vec = (contA % 4 == 0) && (contB % 4 == 0) && (lda % 4 == 0) && (ldb % 4 == 0) &&
                    aligned16(A) && aligned16(B);
-  dim3 grid(ceil_div(N, GBN), ceil_div(M, GBM), splits);
+  dim3 grid(p.nt(N), p.mt(M), p.splits);
   // profile key "<kernel symbol>|<phase>": the symbol part matches rocprofv3's kernel names
   static const char* lay[2] = {"RK", "KR"};
-  char key[96];
-  snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d>|%s", lay[AL], lay[BL], vec ? 4 : 1, name);
+  char key[112];
+  snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d,%d,%d>|%s", lay[AL], lay[BL], vec ? 4 : 1,
+           p.bm, p.bn, name);
   ProfScope ps(c, key, 2.0 * M * N * (double)K, 0.0);
   if (vec)
-    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, 4>), grid, dim3(GNT), 0, c->stream, g);
+    gemm_dispatch<AL, BL, 4>(p, grid, c->stream, g);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, 1>), grid, dim3(GNT), 0, c->stream, g);
+    gemm_dispatch<AL, BL, 1>(p, grid, c->stream, g);
   HIP_TRY(hipGetLastError());
-}
-
-// weight-grad split: aim for ~2 blocks per CU, >= 256 k per split
-static int wgrad_splits(int M, int N, int K) {
-  const int tiles = ceil_div(M, GBM) * ceil_div(N, GBN);
-  int s = std::max(1, 512 / tiles);
-  s = std::min(s, std::max(1, K / 256));
-  return std::min(s, 64);
+  return p;
 }
 
 // ====================================================================== building blocks
 static const float* P(ddpg_ctx* c, const float* base, const Tensor& t) { return base + t.off; }
 
 // Actor forward (networks.py:51-63) on [B][ldS] states.
-// h1 is always materialised (input of layer 2); h2 only when store_h2.
+// h1 is always materialised (input of layer 2); h2 only when h2 != nullptr.
 static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, float* h1,
                       float* h2, float* o, float* mu) {
   const Layout& L = c->L;
@@ -281,8 +355,7 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
   e.ldo = c->ldAH1;
   e.bias = P(c, base, L.a[AB1]);
   e.act = 1;
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.a[AW1]), c->AH1, B, c->AH1, c->S,
-                          e);
+  gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.a[AW1]), c->AH1, B, c->AH1, c->S, e);
   e = epi_none();
   e.out = h2;
   e.ldo = c->ldAH2;
@@ -293,35 +366,31 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
   e.proj_sn = c->A;
   e.proj_sa = 1;
   e.proj_out = c->ppart;
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd_head", h1, c->ldAH1, P(c, base, L.a[AW2]), c->AH2, B,
-                          c->AH2, c->AH1, e);
-  const int NT = ceil_div(c->AH2, GBN);
-  {
-    ProfScope ps(c, "actor_out", 0, 0);
-    hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
-                       c->ppart, NT, B, c->A, c->cfg.action_scale, o, mu, c->ldA);
-    HIP_TRY(hipGetLastError());
-  }
+  GemmPlan pl = gemm_launch<L_RK, L_KR>(c, "fwd_head", h1, c->ldAH1, P(c, base, L.a[AW2]),
+                                        c->AH2, B, c->AH2, c->AH1, e);
+  ProfScope ps(c, "actor_out", 0, 0);
+  hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
+                     c->ppart, pl.nt(c->AH2), B, c->A, c->cfg.action_scale, o, mu, c->ldA);
+  HIP_TRY(hipGetLastError());
 }
 
 // Critic first layer + hidden layer (networks.py:147-161).  mode:
 //   0: store h (train), proj(Wo) -> qpart
 //   1: proj(Wo) -> qpart only (predict / target)
 //   2: dh_pre = Wo[j] * elu'(h) -> dhp_out (action-gradient path, grad_ys = 1)
-static void critic_fwd(ddpg_ctx* c, const float* base, const float* s, const float* a, int B,
-                       float* cat, float* h_out, int mode, float* dhp_out) {
+// Returns the number of qpart slabs (modes 0/1).
+static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const float* a, int B,
+                      float* cat, float* h_out, int mode, float* dhp_out) {
   const Layout& L = c->L;
   GemmEpi e = epi_none();
   e.out = cat;
   e.ldo = c->ldC;
   e.bias = P(c, base, L.c[CBS]);
   e.act = 1;
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1, c->S,
-                          e);
+  gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1, c->S, e);
   e.out = cat + c->CH1;
   e.bias = P(c, base, L.c[CBA]);
-  gemm_launch<L_RK, L_KR>(c, "gemm_fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1, c->A,
-                          e);
+  gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1, c->A, e);
   e = epi_none();
   e.bias = P(c, base, L.c[CBH]);
   e.act = 1;
@@ -339,8 +408,9 @@ static void critic_fwd(ddpg_ctx* c, const float* base, const float* s, const flo
     e.proj_sa = 0;
     e.proj_out = c->qpart;
   }
-  gemm_launch<L_RK, L_KR>(c, mode == 2 ? "gemm_fwd" : "gemm_fwd_head", cat, c->ldC,
-                          P(c, base, L.c[CWH]), c->CH2, B, c->CH2, 2 * c->CH1, e);
+  GemmPlan pl = gemm_launch<L_RK, L_KR>(c, mode == 2 ? "fwd_dhead" : "fwd_head", cat, c->ldC,
+                                        P(c, base, L.c[CWH]), c->CH2, B, c->CH2, 2 * c->CH1, e);
+  return pl.nt(c->CH2);
 }
 
 // dQ/da of the (already updated) online critic at (s, a): networks.py:143.
@@ -358,43 +428,39 @@ static void critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int 
   e.proj_sn = 1;
   e.proj_sa = c->CH1;
   e.proj_out = c->ppart;
-  // B operand = Wh[H1:2H1, :]^T  (NK: element (k=j, n=i) at Wh[(H1+i)*H2 + j])
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp2, c->ldCH2,
-                          P(c, c->theta, L.c[CWH]) + (size_t)c->CH1 * c->CH2, c->CH2, B, c->CH1, c->CH2,
-                          e);
+  // B operand = Wh[CH1:2CH1, :]^T  (NK: element (k=j, n=i) at Wh[(CH1+i)*CH2 + j])
+  GemmPlan pl = gemm_launch<L_RK, L_RK>(c, "dx_da", c->dhp2, c->ldCH2,
+                                        P(c, c->theta, L.c[CWH]) + (size_t)c->CH1 * c->CH2,
+                                        c->CH2, B, c->CH1, c->CH2, e);
   ProfScope ps(c, "action_grad", 0, 0);
   hipLaunchKernelGGL(action_grad_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
-                     c->ppart, ceil_div(c->CH1, GBN), B, c->A, B, o, c->ldA,
-                     c->cfg.action_scale, da, dz3);
-  HIP_TRY(hipGetLastError());
-}
-
-static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
-  long long tot = 0;
-  for (int i = 0; i < tab.nseg; ++i) {
-    tab.start[i] = tot;
-    tot += (long long)tab.seg[i].rows * tab.seg[i].cols;
-  }
-  tab.start[tab.nseg] = tot;
-  double bytes = 0;
-  for (int i = 0; i < tab.nseg; ++i)
-    bytes += (double)tab.seg[i].rows * tab.seg[i].cols * 4.0 * (tab.seg[i].nslab + 1);
-  ProfScope ps(c, name, 0, bytes);
-  int blocks = (int)std::min<long long>(2048, (tot + 255) / 256);
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(std::max(1, blocks)), dim3(256), 0, c->stream, tab);
+                     c->ppart, pl.nt(c->CH1), B, c->A, B, o, c->ldA, c->cfg.action_scale, da,
+                     dz3);
   HIP_TRY(hipGetLastError());
 }
 
 static void add_seg(ReduceTable& t, const float* src, float* dst, long long stride, int nslab,
-                    int rows, int cols, int src_ld) {
+                    long long count) {
   ReduceSeg& s = t.seg[t.nseg++];
   s.src = src;
   s.dst = dst;
   s.slab_stride = stride;
   s.nslab = nslab;
-  s.rows = rows;
-  s.cols = cols;
-  s.src_ld = src_ld;
+  s.count = count;
+  s.vec4 = (count % 4 == 0) && (stride % 4 == 0) && aligned16(src) && aligned16(dst);
+}
+
+static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
+  long long maxc = 1;
+  double bytes = 0;
+  for (int i = 0; i < tab.nseg; ++i) {
+    maxc = std::max(maxc, tab.seg[i].count);
+    bytes += (double)tab.seg[i].count * 4.0 * (tab.seg[i].nslab + 1);
+  }
+  ProfScope ps(c, name, 0, bytes);
+  const int bx = (int)std::min<long long>(512, std::max<long long>(1, (maxc / 4 + 255) / 256));
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, tab.nseg), dim3(256), 0, c->stream, tab);
+  HIP_TRY(hipGetLastError());
 }
 
 static void allreduce(ddpg_ctx* c, float* buf, size_t n) {
@@ -404,29 +470,38 @@ static void allreduce(ddpg_ctx* c, float* buf, size_t n) {
   if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
 }
 
-static void adam_launch(ddpg_ctx* c, int net) {
+// TF ApplyAdam over one network's flat region.  advance: also advance its
+// beta powers right after (1:1 API path); the fused step advances both in
+// the soft-update kernel instead.
+static void adam_launch(ddpg_ctx* c, int net, bool advance) {
   const size_t b = net == 0 ? c->L.actor_begin : c->L.critic_begin;
   const size_t e = net == 0 ? c->L.actor_end : c->L.critic_end;
   const long long n = (long long)(e - b);
   const float lr = net == 0 ? c->cfg.actor_lr : c->cfg.critic_lr;
-  int blocks = (int)std::min<long long>(2048, std::max<long long>(1, (n / 4 + 255) / 256));
-  ProfScope ps(c, "adam", 0, 28.0 * n);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
-                     c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net,
-                     c->dcounter + net, lr, c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon);
-  HIP_TRY(hipGetLastError());
+  int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
+  {
+    ProfScope ps(c, "adam", 0, 28.0 * n);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
+                       c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net, lr,
+                       c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon);
+    HIP_TRY(hipGetLastError());
+  }
+  if (advance) {
+    hipLaunchKernelGGL(advance_powers_kernel, dim3(1), dim3(1), 0, c->stream, c->dpw, 1 << net,
+                       c->cfg.beta1, c->cfg.beta2);
+    HIP_TRY(hipGetLastError());
+  }
 }
 
 // Critic update on rows already in c->s / c->a with targets in c->y.
 // networks.py:130-137,170-175 (+ RCCL sum over ranks for world > 1).
-static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
+static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused) {
   const Layout& L = c->L;
-  critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
+  const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
   {
     ProfScope ps(c, "critic_loss", 0, 0);
-    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->stream, c->qpart,
-                       ceil_div(c->CH2, GBN), B, P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q,
-                       c->dq, c->dstats, c->dacc);
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->stream, c->qpart, nq, B,
+                       P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq, c->dstats, c->dacc);
     HIP_TRY(hipGetLastError());
   }
   const int nchunk = ceil_div(B, kHeadRows);
@@ -441,15 +516,13 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
     HIP_TRY(hipGetLastError());
   }
   // dWh = cat^T . dh_pre   (split-K slabs)
-  const int sWh = std::min(c->split_cap_Wh, wgrad_splits(2 * c->CH1, c->CH2, B));
   GemmEpi e = epi_none();
   e.out = c->slab_Wh;
   e.ldo = c->CH2;
   e.out_split_stride = (long long)2 * c->CH1 * c->CH2;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1, c->CH2, B,
-                          e, sWh);
+  GemmPlan pWh = gemm_launch<L_KR, L_KR>(c, "wgrad", c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1,
+                                         c->CH2, B, e, 0, c->split_cap_Wh);
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
-  const int mt = ceil_div(B, GBM);
   e = epi_none();
   e.post = 1;
   e.aux = c->cat;
@@ -458,59 +531,52 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b) {
   e.ldo = c->ldC;
   e.colsum = c->colpart;
   e.ld_colsum = 2 * c->CH1;
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]), c->CH2, B,
-                          2 * c->CH1, c->CH2, e);
+  GemmPlan pdc = gemm_launch<L_RK, L_RK>(c, "dx", c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]),
+                                         c->CH2, B, 2 * c->CH1, c->CH2, e);
+  const int mt = pdc.mt(B);
   // dWs = s^T . dcs ; dWa = a^T . dca
-  const int sWs = std::min(c->split_cap_Ws, wgrad_splits(c->S, c->CH1, B));
   e = epi_none();
   e.out = c->slab_Ws;
   e.ldo = c->CH1;
   e.out_split_stride = (long long)c->S * c->CH1;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, e, sWs);
-  const int sWa = std::min(c->split_cap_Wa, wgrad_splits(c->A, c->CH1, B));
+  GemmPlan pWs = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1,
+                                         B, e, 0, c->split_cap_Ws);
   e.out = c->slab_Wa;
   e.out_split_stride = (long long)c->A * c->CH1;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A, c->CH1, B,
-                          e, sWa);
+  GemmPlan pWa = gemm_launch<L_KR, L_KR>(c, "wgrad", c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A,
+                                         c->CH1, B, e, 0, c->split_cap_Wa);
   // gather every critic gradient into the flat grad buffer
   float* G = c->grad;
   ReduceTable tab;
   tab.nseg = 0;
-  const long long kps_unused = 0;
-  (void)kps_unused;
-  auto gsplits = [&](int s, int K) {  // effective split count used by gemm_launch
-    int kps = rup(std::max(1, ceil_div(K, s)), GBK);
-    return std::max(1, ceil_div(K, kps));
-  };
-  add_seg(tab, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1, gsplits(sWs, B), c->S,
-          c->CH1, c->CH1);
-  add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, 1, c->CH1, 0);
-  add_seg(tab, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1, gsplits(sWa, B), c->A,
-          c->CH1, c->CH1);
-  add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, 1, c->CH1, 0);
-  add_seg(tab, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->CH1 * c->CH2, gsplits(sWh, B),
-          2 * c->CH1, c->CH2, c->CH2);
-  add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, 1, c->CH2, 0);
-  add_seg(tab, part_dWo, G + L.c[CWO].off, c->CH2, nchunk, 1, c->CH2, 0);
-  add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1, 1, 0);
+  add_seg(tab, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1, pWs.splits,
+          (long long)c->S * c->CH1);
+  add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, c->CH1);
+  add_seg(tab, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1, pWa.splits,
+          (long long)c->A * c->CH1);
+  add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, c->CH1);
+  add_seg(tab, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->CH1 * c->CH2, pWh.splits,
+          (long long)2 * c->CH1 * c->CH2);
+  add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, c->CH2);
+  add_seg(tab, part_dWo, G + L.c[CWO].off, c->CH2, nchunk, c->CH2);
+  add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.critic_begin, L.critic_end - L.critic_begin);
-  adam_launch(c, 1);
+  adam_launch(c, 1, !fused);
 }
 
 // Actor update given dz3 (= TanhGrad chain of -dQ/da) and the forward
 // activations h1, h2 of c->s.  networks.py:39-47,71-75.
-static void actor_train_dev(ddpg_ctx* c, int B) {
+static void actor_train_dev(ddpg_ctx* c, int B, bool fused) {
   const Layout& L = c->L;
   float* G = c->grad;
-  const int mt = ceil_div(B, GBM);
   // dW3 = h2^T . dz3
-  const int sW3 = std::min(c->split_cap_W3, wgrad_splits(c->AH2, c->A, B));
   GemmEpi e = epi_none();
   e.out = c->slab_W3;
   e.ldo = c->A;
   e.out_split_stride = (long long)c->AH2 * c->A;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, e, sW3);
+  GemmPlan pW3 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A,
+                                         B, e, 0, c->split_cap_W3);
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
   e = epi_none();
   e.post = 1;
@@ -520,18 +586,18 @@ static void actor_train_dev(ddpg_ctx* c, int B) {
   e.ldo = c->ldAH2;
   e.colsum = c->colpart;
   e.ld_colsum = c->AH2;
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A, B, c->AH2,
-                          c->A, e);
+  GemmPlan pz2 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A,
+                                         B, c->AH2, c->A, e);
+  const int mt2 = pz2.mt(B);
   // dW2 = h1^T . dz2
-  const int sW2 = std::min(c->split_cap_W2, wgrad_splits(c->AH1, c->AH2, B));
   e = epi_none();
   e.out = c->slab_W2;
   e.ldo = c->AH2;
   e.out_split_stride = (long long)c->AH1 * c->AH2;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1, c->AH2, B, e,
-                          sW2);
+  GemmPlan pW2 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1,
+                                         c->AH2, B, e, 0, c->split_cap_W2);
   // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
-  float* colpart1 = c->colpart + (size_t)mt * c->AH2;
+  float* colpart1 = c->colpart + (size_t)mt2 * c->AH2;
   e = epi_none();
   e.post = 1;
   e.aux = c->h1;
@@ -540,52 +606,54 @@ static void actor_train_dev(ddpg_ctx* c, int B) {
   e.ldo = c->ldAH1;
   e.colsum = colpart1;
   e.ld_colsum = c->AH1;
-  gemm_launch<L_RK, L_RK>(c, "gemm_dx", c->dz2, c->ldAH2, P(c, c->theta, L.a[AW2]), c->AH2, B,
-                          c->AH1, c->AH2, e);
+  GemmPlan pz1 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz2, c->ldAH2, P(c, c->theta, L.a[AW2]),
+                                         c->AH2, B, c->AH1, c->AH2, e);
   // dW1 = s^T . dz1
-  const int sW1 = std::min(c->split_cap_W1, wgrad_splits(c->S, c->AH1, B));
   e = epi_none();
   e.out = c->slab_W1;
   e.ldo = c->AH1;
   e.out_split_stride = (long long)c->S * c->AH1;
-  gemm_launch<L_KR, L_KR>(c, "gemm_wgrad", c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1, B, e, sW1);
-
-  auto gsplits = [&](int s, int K) {
-    int kps = rup(std::max(1, ceil_div(K, s)), GBK);
-    return std::max(1, ceil_div(K, kps));
-  };
+  GemmPlan pW1 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1,
+                                         B, e, 0, c->split_cap_W1);
   ReduceTable tab;
   tab.nseg = 0;
-  add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1, gsplits(sW1, B), c->S, c->AH1,
-          c->AH1);
-  add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, mt, 1, c->AH1, 0);
-  add_seg(tab, c->slab_W2, G + L.a[AW2].off, (long long)c->AH1 * c->AH2, gsplits(sW2, B), c->AH1,
-          c->AH2, c->AH2);
-  add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt, 1, c->AH2, 0);
-  add_seg(tab, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A, gsplits(sW3, B), c->AH2,
-          c->A, c->A);
+  add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1, pW1.splits,
+          (long long)c->S * c->AH1);
+  add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, pz1.mt(B), c->AH1);
+  add_seg(tab, c->slab_W2, G + L.a[AW2].off, (long long)c->AH1 * c->AH2, pW2.splits,
+          (long long)c->AH1 * c->AH2);
+  add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt2, c->AH2);
+  add_seg(tab, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A, pW3.splits,
+          (long long)c->AH2 * c->A);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.actor_begin, L.actor_end - L.actor_begin);
-  adam_launch(c, 0);
+  adam_launch(c, 0, !fused);
 }
 
-static void soft_update_dev(ddpg_ctx* c, int mask) {
+// Soft target update (networks.py:34-37) over the selected networks; pw_mask
+// additionally advances those networks' Adam beta powers (fused step).
+static void soft_update_dev(ddpg_ctx* c, int mask, int pw_mask) {
   const float tau = c->cfg.tau;
   const float omt = (float)(1.0 - (double)tau);
-  auto run = [&](size_t b, size_t e) {
-    const long long n = (long long)(e - b);
-    int blocks = (int)std::min<long long>(2048, std::max<long long>(1, (n / 4 + 255) / 256));
-    ProfScope ps(c, "soft_update", 0, 12.0 * n);
-    hipLaunchKernelGGL(soft_update_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
-                       c->target + b, n, tau, omt);
-    HIP_TRY(hipGetLastError());
-  };
-  if ((mask & DDPG_SOFT_ACTOR) && (mask & DDPG_SOFT_CRITIC))
-    run(c->L.actor_begin, c->L.critic_end);
-  else if (mask & DDPG_SOFT_ACTOR)
-    run(c->L.actor_begin, c->L.actor_end);
-  else if (mask & DDPG_SOFT_CRITIC)
-    run(c->L.critic_begin, c->L.critic_end);
+  size_t b, e;
+  if ((mask & DDPG_SOFT_ACTOR) && (mask & DDPG_SOFT_CRITIC)) {
+    b = c->L.actor_begin;
+    e = c->L.critic_end;
+  } else if (mask & DDPG_SOFT_ACTOR) {
+    b = c->L.actor_begin;
+    e = c->L.actor_end;
+  } else if (mask & DDPG_SOFT_CRITIC) {
+    b = c->L.critic_begin;
+    e = c->L.critic_end;
+  } else {
+    return;
+  }
+  const long long n = (long long)(e - b);
+  int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
+  ProfScope ps(c, "soft_update", 0, 12.0 * n);
+  hipLaunchKernelGGL(soft_update_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
+                     c->target + b, n, tau, omt, c->dpw, pw_mask, c->cfg.beta1, c->cfg.beta2);
+  HIP_TRY(hipGetLastError());
 }
 
 // One full learner step (ddpg.py:86-113) on rows already gathered into
@@ -594,23 +662,23 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   const Layout& L = c->L;
   // target_q = critic.predict_target(s2, actor.predict_target(s2))  ddpg.py:90
   actor_fwd(c, c->target, c->s2, B, c->th1, nullptr, nullptr, c->ta2);
-  critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr);
+  const int nq = critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr);
   {
     ProfScope ps(c, "td_target", 0, 0);
     hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
-                       ceil_div(c->CH2, GBN), B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t,
-                       c->cfg.gamma, c->y);
+                       nq, B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t, c->cfg.gamma,
+                       c->y);
     HIP_TRY(hipGetLastError());
   }
   // critic.train(s, a, y)  ddpg.py:100
-  critic_train_dev(c, B, inv_b);
+  critic_train_dev(c, B, inv_b, true);
   // a_outs = actor.predict(s); grads = critic.action_gradients(s, a_outs)  ddpg.py:106-107
   actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu);
   critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);
   // actor.train(s, grads[0])  ddpg.py:109  (forward above reused: same params)
-  actor_train_dev(c, B);
-  // actor/critic.update_target_network()  ddpg.py:112-113
-  soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC);
+  actor_train_dev(c, B, true);
+  // actor/critic.update_target_network()  ddpg.py:112-113 (+ both Adam power updates)
+  soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC, 3);
 }
 
 // ====================================================================== helpers
@@ -664,6 +732,11 @@ static void ctx_free(ddpg_ctx* c) {
   for (int i = 0; i < kSlotRing; ++i)
     if (c->slot_ev[i]) (void)hipEventDestroy(c->slot_ev[i]);
   if (c->h_slots) (void)hipHostFree(c->h_slots);
+  for (auto& g : c->gslot) {
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (g.h_idx) (void)hipHostFree(g.h_idx);
+    if (g.done) (void)hipEventDestroy(g.done);
+  }
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc})
     if (p) (void)hipFree(p);
@@ -748,16 +821,17 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
 
     // activation workspace
     const size_t B = (size_t)c->Bmax;
-    const int NTP = std::max(ceil_div(c->AH2, GBN), ceil_div(c->CH1, GBN));
-    const int NTQ = ceil_div(c->CH2, GBN);
-    const int mt = ceil_div(c->Bmax, GBM);
+    const int NTP = std::max(ceil_div(c->AH2, 64), ceil_div(c->CH1, 64));
+    const int NTQ = ceil_div(c->CH2, 64);
+    const int mt = ceil_div(c->Bmax, 64);
     const int nchunk = ceil_div(c->Bmax, kHeadRows);
-    c->split_cap_W1 = wgrad_splits(c->S, c->AH1, c->Bmax);
-    c->split_cap_W2 = wgrad_splits(c->AH1, c->AH2, c->Bmax);
-    c->split_cap_W3 = wgrad_splits(c->AH2, c->A, c->Bmax);
-    c->split_cap_Ws = wgrad_splits(c->S, c->CH1, c->Bmax);
-    c->split_cap_Wa = wgrad_splits(c->A, c->CH1, c->Bmax);
-    c->split_cap_Wh = wgrad_splits(2 * c->CH1, c->CH2, c->Bmax);
+    if (const char* mb = getenv("DDPG_GEMM_MIN_BLOCKS")) g_min_blocks = std::max(1, atoi(mb));
+    c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
+    c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;
+    c->split_cap_W3 = make_plan(c->AH2, c->A, c->Bmax, 0).splits;
+    c->split_cap_Ws = make_plan(c->S, c->CH1, c->Bmax, 0).splits;
+    c->split_cap_Wa = make_plan(c->A, c->CH1, c->Bmax, 0).splits;
+    c->split_cap_Wh = make_plan(2 * c->CH1, c->CH2, c->Bmax, 0).splits;
     struct Req {
       float** p;
       size_t n;
@@ -796,6 +870,11 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     HIP_TRY(hipHostMalloc(&c->h_slots, kSlotRing * B * sizeof(int)));
     for (int i = 0; i < kSlotRing; ++i) HIP_TRY(hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming));
     c->idx_tmp.resize(B * c->world);
+    for (auto& g : c->gslot) {
+      HIP_TRY(hipHostMalloc(&g.h_idx, B * sizeof(int)));
+      HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
+    }
+    if (const char* gv = getenv("DDPG_GRAPH")) c->use_graph = atoi(gv) != 0;
     HIP_TRY(hipDeviceSynchronize());
   });
   if (rc != DDPG_OK) {
@@ -956,9 +1035,9 @@ int ddpg_critic_forward(ddpg_ctx* c, int target, const float* s, const float* a,
     apply_scaler(c, c->s, B);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     const float* base = target ? c->target : c->theta;
-    critic_fwd(c, base, c->s, c->a, B, c->cat, nullptr, 1, nullptr);
+    const int nq = critic_fwd(c, base, c->s, c->a, B, c->cat, nullptr, 1, nullptr);
     hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
-                       ceil_div(c->CH2, GBN), B, P(c, base, c->L.c[CBO]), c->q, 0, nullptr,
+                       nq, B, P(c, base, c->L.c[CBO]), c->q, 0, nullptr,
                        nullptr, 0.f, nullptr);
     HIP_TRY(hipGetLastError());
     download_rows(c, q_out, c->q, 1, B, 1);
@@ -973,7 +1052,7 @@ int ddpg_critic_train(ddpg_ctx* c, const float* s, const float* a, const float* 
     apply_scaler(c, c->s, B);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     upload_rows(c, c->y, 1, y, B, 1);
-    critic_train_dev(c, B, 1.0f / (float)(B * c->world));
+    critic_train_dev(c, B, 1.0f / (float)(B * c->world), false);
     if (q_pre) download_rows(c, q_pre, c->q, 1, B, 1);
     if (loss) {
       float st[2];
@@ -1008,14 +1087,14 @@ int ddpg_actor_train(ddpg_ctx* c, const float* s, const float* a_gradient, int B
                        c->dain, 1, B, c->A, B, c->o, c->ldA, c->cfg.action_scale, nullptr,
                        c->dz3);
     HIP_TRY(hipGetLastError());
-    actor_train_dev(c, B);
+    actor_train_dev(c, B, false);
     HIP_TRY(hipStreamSynchronize(c->stream));
   });
 }
 
 int ddpg_soft_update(ddpg_ctx* c, int mask) {
   return guard(c, [&] {
-    soft_update_dev(c, mask);
+    soft_update_dev(c, mask, 0);
     HIP_TRY(hipStreamSynchronize(c->stream));
   });
 }
@@ -1060,6 +1139,7 @@ int ddpg_replay_create(int device, int S, int A, int64_t cap, int64_t seed, ddpg
     rb->cap = cap;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&rb->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&rb->last_read, hipEventDisableTiming));
     const size_t c = (size_t)cap;
     HIP_TRY(hipMalloc(&rb->rs, c * S * 4));
     HIP_TRY(hipMalloc(&rb->rs2, c * S * 4));
@@ -1089,6 +1169,7 @@ void ddpg_replay_destroy(ddpg_replay* rb) {
                   (void*)rb->d_slots, (void*)rb->d_tmp})
     if (p) (void)hipFree(p);
   if (rb->stream) (void)hipStreamDestroy(rb->stream);
+  if (rb->last_read) (void)hipEventDestroy(rb->last_read);
   delete rb;
 }
 
@@ -1116,6 +1197,7 @@ static void ring_write(ddpg_replay* rb, int64_t first, int n, const float* s, co
 
 static void replay_flush(ddpg_replay* rb) {
   if (rb->st_n == 0) return;
+  if (rb->last_read) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->last_read, 0));
   ring_write(rb, rb->st_first, rb->st_n, rb->st_s.data(), rb->st_a.data(), rb->st_r.data(),
              rb->st_t.data(), rb->st_s2.data());
   HIP_TRY(hipStreamSynchronize(rb->stream));  // staging is reused after this
@@ -1131,6 +1213,7 @@ int ddpg_replay_add(ddpg_replay* rb, const float* s, const float* a, const float
     int done = 0;
     if (n >= kStageRows) {  // bulk insert: straight from the caller's arrays
       replay_flush(rb);
+      if (rb->last_read) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->last_read, 0));
       std::vector<float> rf(r, r + n), tf(n);
       for (int i = 0; i < n; ++i) tf[i] = t[i] ? 1.f : 0.f;
       // only the last `cap` rows can survive; skip the ones that would be overwritten
@@ -1229,6 +1312,15 @@ int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* 
 }
 
 // ---------------------------------------------------------------- fused step
+static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
+  ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->stream,
+                     c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, c->S, c->A, c->s,
+                     c->s2, c->ldS, c->a, c->ldA, c->r, c->t, c->has_scaler ? c->dmean : nullptr,
+                     c->has_scaler ? c->dscale : nullptr);
+  HIP_TRY(hipGetLastError());
+}
+
 static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg,
                         ddpg_stats* stats) {
   if (rb->S != c->S || rb->A != c->A)
@@ -1237,25 +1329,50 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   if (Bg % c->world) throw einval("global batch %d not divisible by world %d", Bg, c->world);
   const int B = Bg / c->world;
   check_b(c, B);
-  // this rank's slice of the globally drawn positions -> ring slots (pinned)
-  const int si = c->slot_i;
-  c->slot_i = (c->slot_i + 1) % kSlotRing;
-  HIP_TRY(hipEventSynchronize(c->slot_ev[si]));
-  int* hs = c->h_slots + (size_t)si * c->Bmax;
-  const int64_t* mine = idx + (size_t)c->rank * B;
-  for (int i = 0; i < B; ++i) hs[i] = pos_to_slot(rb, mine[i]);
-  HIP_TRY(hipMemcpyAsync(c->d_slots, hs, (size_t)B * sizeof(int), hipMemcpyHostToDevice,
-                         c->stream));
-  HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
-  {
-    ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
-    hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->stream,
-                       c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, c->S, c->A, c->s,
-                       c->s2, c->ldS, c->a, c->ldA, c->r, c->t,
-                       c->has_scaler ? c->dmean : nullptr, c->has_scaler ? c->dscale : nullptr);
-    HIP_TRY(hipGetLastError());
+  const int64_t* mine = idx + (size_t)c->rank * B;  // this rank's slice of the global draw
+  const float inv_b = 1.0f / (float)Bg;
+  // graphs: single-rank, not profiling (RCCL capture and per-kernel events stay eager)
+  if (c->use_graph && c->world == 1 && !c->prof) {
+    auto& g = c->gslot[c->gcur];
+    c->gcur ^= 1;
+    HIP_TRY(hipEventSynchronize(g.done));  // this slot's previous replay has finished
+    for (int i = 0; i < B; ++i) g.h_idx[i] = pos_to_slot(rb, mine[i]);
+    if (!g.exec || g.B != B || g.rb != rb || g.scaler != c->has_scaler) {
+      if (g.exec) HIP_TRY(hipGraphExecDestroy(g.exec));
+      g.exec = nullptr;
+      hipGraph_t graph;
+      HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      try {
+        HIP_TRY(hipMemcpyAsync(c->d_slots, g.h_idx, (size_t)B * sizeof(int),
+                               hipMemcpyHostToDevice, c->stream));
+        gather_launch(c, rb, B);
+        learner_step_dev(c, B, inv_b);
+      } catch (...) {
+        (void)hipStreamEndCapture(c->stream, &graph);
+        throw;
+      }
+      HIP_TRY(hipStreamEndCapture(c->stream, &graph));
+      HIP_TRY(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+      HIP_TRY(hipGraphDestroy(graph));
+      g.B = B;
+      g.rb = rb;
+      g.scaler = c->has_scaler;
+    }
+    HIP_TRY(hipGraphLaunch(g.exec, c->stream));
+    HIP_TRY(hipEventRecord(g.done, c->stream));
+  } else {
+    const int si = c->slot_i;
+    c->slot_i = (c->slot_i + 1) % kSlotRing;
+    HIP_TRY(hipEventSynchronize(c->slot_ev[si]));
+    int* hs = c->h_slots + (size_t)si * c->Bmax;
+    for (int i = 0; i < B; ++i) hs[i] = pos_to_slot(rb, mine[i]);
+    HIP_TRY(hipMemcpyAsync(c->d_slots, hs, (size_t)B * sizeof(int), hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
+    gather_launch(c, rb, B);
+    learner_step_dev(c, B, inv_b);
   }
-  learner_step_dev(c, B, 1.0f / (float)Bg);
+  HIP_TRY(hipEventRecord(rb->last_read, c->stream));
   if (stats) {
     float st[2];
     HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));

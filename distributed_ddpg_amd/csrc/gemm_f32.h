@@ -8,12 +8,13 @@
 //   weight grad  dW = X^T . dY       A: X  [K=B][M=in]  (KR)   B: dY [K=B][N=out]  (KR)
 // Layout codes: RK = operand rows contiguous in k, KR = k-major, rows contiguous.
 //
-// Block tile 128x128x32, 256 threads = 4 waves (2x2), each wave 64x64 =
-// 2x2 MFMA 32x32 tiles.  Both operands are staged k-major into LDS
-// ([k][row], stride 129 when the global source is k-contiguous so that the
-// transposing scalar LDS writes and the MFMA operand reads are both
-// bank-conflict free; stride 128 + ds_write_b128 otherwise).  Register
-// prefetch of tile t+1 overlaps the MFMAs of tile t (one barrier per k-tile).
+// Block tile BM x BN x 32 (BM, BN in {64, 128}), 256 threads = 4 waves (2x2),
+// each wave (BM/2) x (BN/2) = TM x TN MFMA 32x32 tiles.  Both operands are
+// staged k-major into LDS ([k][row], stride BR+1 when the global source is
+// k-contiguous so that the transposing scalar LDS writes and the MFMA operand
+// reads are both bank-conflict free; stride BR + ds_write_b128 otherwise).
+// Register prefetch of tile t+1 overlaps the MFMAs of tile t (one barrier per
+// k-tile).
 //
 // Epilogue (all optional, fused so that no thin layer is a separate pass):
 //   v = acc (+ bias[n]) -> act (elu) -> post:
@@ -30,10 +31,16 @@ namespace ddpg {
 
 enum { L_RK = 0, L_KR = 1 };
 
-constexpr int GBM = 128, GBN = 128, GBK = 32, GNT = 256;
-constexpr int GSMEM = 2 * GBK * (GBM + 1) + 2 * GBK * (GBN + 1);  // 16512 floats
-constexpr int VS_LD = 132;                                        // epilogue tile stride
+constexpr int GBK = 32, GNT = 256;
 constexpr int PROJ_MAX = 32;
+
+template <int BM, int BN>
+struct TileCfg {
+  static constexpr int STAGE = 2 * GBK * (BM + 1) + 2 * GBK * (BN + 1);
+  static constexpr int VS_LD = BN + 4;
+  static constexpr int EPI = (BM / 2) * VS_LD + BN * PROJ_MAX + GNT;
+  static constexpr int SMEM = STAGE > EPI ? STAGE : EPI;
+};
 
 struct GemmEpi {
   float* out;
@@ -61,11 +68,13 @@ struct GemmArgs {
 };
 
 // ---------------------------------------------------------------- staging
-template <int L, int VEC>
+// One operand tile of BR rows x GBK k, global -> registers -> LDS [k][row].
+template <int L, int VEC, int BR>
 struct Stage {
   static constexpr int PAD = (L == L_RK) ? 1 : 0;
-  static constexpr int LS = GBM + PAD;                // LDS row stride ([k][row])
-  static constexpr int NV = (GBM * GBK) / (GNT * VEC);  // vectors per thread
+  static constexpr int LS = BR + PAD;                  // LDS row stride ([k][row])
+  static constexpr int NV = (BR * GBK) / (GNT * VEC);  // vectors per thread
+  static constexpr int RQ = BR / 4;                    // float4 per k-row (KR)
   float v[NV * VEC];
 
   DDPG_DEV void load(const float* __restrict__ P, int ld, int R, int kend, int r0, int k0,
@@ -73,8 +82,8 @@ struct Stage {
     if constexpr (L == L_RK && VEC == 4) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, r = f >> 3, kq = f & 7;
-        int gr = r0 + r, gk = k0 + 4 * kq;
+        const int f = i * GNT + tid, r = f >> 3, kq = f & 7;
+        const int gr = r0 + r, gk = k0 + 4 * kq;
         float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gr < R && gk < kend) x = *reinterpret_cast<const float4*>(P + (size_t)gr * ld + gk);
         v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
@@ -82,15 +91,15 @@ struct Stage {
     } else if constexpr (L == L_RK) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, r = f >> 5, k = f & 31;
-        int gr = r0 + r, gk = k0 + k;
+        const int f = i * GNT + tid, r = f >> 5, k = f & 31;
+        const int gr = r0 + r, gk = k0 + k;
         v[i] = (gr < R && gk < kend) ? P[(size_t)gr * ld + gk] : 0.f;
       }
     } else if constexpr (VEC == 4) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, k = f >> 5, rq = f & 31;
-        int gk = k0 + k, gr = r0 + 4 * rq;
+        const int f = i * GNT + tid, k = f / RQ, rq = f % RQ;
+        const int gk = k0 + k, gr = r0 + 4 * rq;
         float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gk < kend && gr < R) x = *reinterpret_cast<const float4*>(P + (size_t)gk * ld + gr);
         v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
@@ -98,8 +107,8 @@ struct Stage {
     } else {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, k = f >> 7, r = f & 127;
-        int gk = k0 + k, gr = r0 + r;
+        const int f = i * GNT + tid, k = f / BR, r = f % BR;
+        const int gk = k0 + k, gr = r0 + r;
         v[i] = (gk < kend && gr < R) ? P[(size_t)gk * ld + gr] : 0.f;
       }
     }
@@ -109,27 +118,27 @@ struct Stage {
     if constexpr (L == L_RK && VEC == 4) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, r = f >> 3, kq = f & 7;
+        const int f = i * GNT + tid, r = f >> 3, kq = f & 7;
 #pragma unroll
         for (int j = 0; j < 4; ++j) lds[(4 * kq + j) * LS + r] = v[4 * i + j];
       }
     } else if constexpr (L == L_RK) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, r = f >> 5, k = f & 31;
+        const int f = i * GNT + tid, r = f >> 5, k = f & 31;
         lds[k * LS + r] = v[i];
       }
     } else if constexpr (VEC == 4) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, k = f >> 5, rq = f & 31;
+        const int f = i * GNT + tid, k = f / RQ, rq = f % RQ;
         *reinterpret_cast<float4*>(lds + k * LS + 4 * rq) =
             make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int f = i * GNT + tid, k = f >> 7, r = f & 127;
+        const int f = i * GNT + tid, k = f / BR, r = f % BR;
         lds[k * LS + r] = v[i];
       }
     }
@@ -137,12 +146,15 @@ struct Stage {
 };
 
 // ---------------------------------------------------------------- kernel
-template <int AL, int BL, int VEC>
+template <int AL, int BL, int VEC, int BM, int BN>
 __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float smem[GSMEM];
-  using SA = Stage<AL, VEC>;
-  using SB = Stage<BL, VEC>;
+  using TC = TileCfg<BM, BN>;
+  __shared__ __attribute__((aligned(16))) float smem[TC::SMEM];
+  using SA = Stage<AL, VEC, BM>;
+  using SB = Stage<BL, VEC, BN>;
   constexpr int LSA = SA::LS, LSB = SB::LS;
+  constexpr int TM = BM / 64, TN = BN / 64;  // MFMA tiles per wave
+  constexpr int WR = BM / 2, WC = BN / 2;    // wave tile
   float* const As0 = smem;
   float* const Bs0 = smem + 2 * GBK * LSA;
 
@@ -150,16 +162,16 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, li = lane & 31;
-  const int n0 = blockIdx.x * GBN, m0 = blockIdx.y * GBM, z = blockIdx.z;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, z = blockIdx.z;
   const int kbeg = z * g.kps;
   const int kend = min(g.K, kbeg + g.kps);
   const int nk = kend > kbeg ? (kend - kbeg + GBK - 1) / GBK : 0;
 
-  f32x16 acc[2][2];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -178,17 +190,21 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
         sa.load(g.A, g.lda, g.M, kend, m0, kbeg + (t + 1) * GBK, tid);
         sb.load(g.B, g.ldb, g.N, kend, n0, kbeg + (t + 1) * GBK, tid);
       }
-      const float* a_s = As0 + cur * GBK * LSA + wm * 64 + li;
-      const float* b_s = Bs0 + cur * GBK * LSB + wn * 64 + li;
+      const float* a_s = As0 + cur * GBK * LSA + wm * WR + li;
+      const float* b_s = Bs0 + cur * GBK * LSB + wn * WC + li;
 #pragma unroll
       for (int kk = 0; kk < GBK / 2; ++kk) {
         const int k = 2 * kk + h;
-        const float a0 = a_s[k * LSA], a1 = a_s[k * LSA + 32];
-        const float b0 = b_s[k * LSB], b1 = b_s[k * LSB + 32];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        float av[TM], bv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[i] = a_s[k * LSA + 32 * i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bv[j] = b_s[k * LSB + 32 * j];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
       }
       if (more) {
         sa.store(As0 + (cur ^ 1) * GBK * LSA, tid);
@@ -203,16 +219,16 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
   const int M = g.M, N = g.N;
   float* outp = e.out ? e.out + (size_t)z * e.out_split_stride : nullptr;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < TM; ++i) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + li;
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WC + j * 32 + li;
       const bool nok = n < N;
       const float bn = (nok && e.bias) ? e.bias[n] : 0.f;
       const float pwn = (nok && e.post == 2) ? e.pw[n] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         float v = acc[i][j][r];
         if (nok && m < M) {
           if (e.bias) v = __fadd_rn(v, bn);
@@ -230,44 +246,49 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
 
   if (!e.colsum && !e.proj_out) return;
 
-  // Row-wise reductions through LDS, 64 tile rows per pass.
-  float* Vs = smem;                 // [64][VS_LD]
-  float* Wps = smem + 64 * VS_LD;   // [128][PN]
-  float* red = Wps + GBN * PROJ_MAX;  // [256]
+  // Row-wise reductions through LDS, WR tile rows (one wave row) per pass.
+  constexpr int VS_LD = TC::VS_LD;
+  float* Vs = smem;                      // [WR][VS_LD]
+  float* Wps = smem + WR * VS_LD;        // [BN][PN]
+  float* red = Wps + BN * PROJ_MAX;      // [GNT]
   const int PN = (e.proj_n + 3) & ~3;
   if (e.proj_out) {
-    for (int idx = tid; idx < GBN * PN; idx += GNT) {
+    for (int idx = tid; idx < BN * PN; idx += GNT) {
       const int nl = idx / PN, a = idx - nl * PN, n = n0 + nl;
       Wps[idx] = (n < N && a < e.proj_n) ? e.proj[(size_t)n * e.proj_sn + (size_t)a * e.proj_sa]
                                           : 0.f;
     }
   }
+  constexpr int CG = GNT / BN;  // column-sum row groups
   float csum = 0.f;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if (wm == pass) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rl = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            Vs[rl * VS_LD + wn * 64 + j * 32 + li] = acc[i][j][r];
+            Vs[rl * VS_LD + wn * WC + j * 32 + li] = acc[i][j][r];
           }
     }
     __syncthreads();
     if (e.colsum) {
-      const int col = tid & 127, rh = tid >> 7;
-#pragma unroll 8
-      for (int rr = 0; rr < 32; ++rr) csum += Vs[(rh * 32 + rr) * VS_LD + col];
+      const int col = tid % BN, grp = tid / BN;
+#pragma unroll 4
+      for (int rr = grp; rr < WR; rr += CG) csum += Vs[rr * VS_LD + col];
     }
     if (e.proj_out) {
       const int PG = PN >> 2;
-      for (int p = tid; p < 64 * PG; p += GNT) {
-        const int row = p & 63, ag = p >> 6;
+      for (int p = tid; p < WR * PG; p += GNT) {
+        const int row = p % WR, ag = p / WR;
         float4 ap = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int n4 = 0; n4 < GBN / 4; ++n4) {
+        // partial unroll: a full unroll makes every Wps load invariant in p
+        // and the compiler hoists them all into registers (spills at BN=64)
+#pragma unroll 2
+        for (int n4 = 0; n4 < BN / 4; ++n4) {
           const float4 vv = *reinterpret_cast<const float4*>(Vs + row * VS_LD + 4 * n4);
           const float vq[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
@@ -279,7 +300,7 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
             ap.w = fmaf(vq[q], w.w, ap.w);
           }
         }
-        const int m = m0 + pass * 64 + row;
+        const int m = m0 + pass * WR + row;
         if (m < M) {
           float* po = e.proj_out + ((size_t)blockIdx.x * M + m) * e.proj_n;
           const float av[4] = {ap.x, ap.y, ap.z, ap.w};
@@ -294,10 +315,12 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f32_kernel(GemmArgs g) {
   if (e.colsum) {
     red[tid] = csum;
     __syncthreads();
-    if (tid < 128) {
+    if (tid < BN) {
+      float s = 0.f;
+#pragma unroll
+      for (int gi = 0; gi < CG; ++gi) s += red[tid + gi * BN];
       const int n = n0 + tid;
-      if (n < N)
-        e.colsum[((size_t)z * gridDim.y + blockIdx.y) * e.ld_colsum + n] = red[tid] + red[tid + 128];
+      if (n < N) e.colsum[((size_t)z * gridDim.y + blockIdx.y) * e.ld_colsum + n] = s;
     }
   }
 }

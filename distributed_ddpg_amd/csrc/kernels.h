@@ -186,35 +186,46 @@ __global__ void action_grad_kernel(const float* __restrict__ part, int NT, int B
 }
 
 // ---------------------------------------------------------------- reductions
+// dst[i] = sum_k src[k * slab_stride + i], i < count  (deterministic order).
+// Split-K weight-gradient slabs, bias column-sum partials and critic-head
+// partials all have this shape.  blockIdx.y selects the segment.
 struct ReduceSeg {
   const float* src;
   float* dst;
   long long slab_stride;  // floats between slabs
+  long long count;
   int nslab;
-  int rows, cols;         // dst region [rows][cols] (contiguous)
-  int src_ld;             // row stride inside a slab
+  int vec4;               // count, stride and pointers allow float4
 };
 constexpr int MAX_SEGS = 12;
 struct ReduceTable {
   ReduceSeg seg[MAX_SEGS];
-  long long start[MAX_SEGS + 1];
   int nseg;
 };
 
-// dst = sum over slabs (deterministic order).
 __global__ void reduce_slabs_kernel(ReduceTable tab) {
-  const long long total = tab.start[tab.nseg];
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    int s = 0;
-    while (i >= tab.start[s + 1]) ++s;
-    const ReduceSeg& g = tab.seg[s];
-    const long long li = i - tab.start[s];
-    const int row = (int)(li / g.cols), col = (int)(li - (long long)row * g.cols);
-    const float* p = g.src + (size_t)row * g.src_ld + col;
-    float acc = 0.f;
-    for (int k = 0; k < g.nslab; ++k) acc += p[(size_t)k * g.slab_stride];
-    g.dst[li] = acc;
+  const ReduceSeg g = tab.seg[blockIdx.y];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long tid0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g.vec4) {
+    const long long n4 = g.count >> 2;
+    const long long s4 = g.slab_stride >> 2;
+    const float4* src = reinterpret_cast<const float4*>(g.src);
+    float4* dst = reinterpret_cast<float4*>(g.dst);
+    for (long long i = tid0; i < n4; i += stride) {
+      float4 acc = src[i];
+      for (int k = 1; k < g.nslab; ++k) {
+        const float4 x = src[i + k * s4];
+        acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+      }
+      dst[i] = acc;
+    }
+  } else {
+    for (long long i = tid0; i < g.count; i += stride) {
+      float acc = g.src[i];
+      for (int k = 1; k < g.nslab; ++k) acc += g.src[i + k * g.slab_stride];
+      g.dst[i] = acc;
+    }
   }
 }
 
@@ -227,8 +238,8 @@ __global__ void reduce_slabs_kernel(ReduceTable tab) {
 // advances them (b1p *= b1, b2p *= b2), i.e. the AdamOptimizer._finish update.
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ g, long long n,
-                            float* __restrict__ pw, unsigned* __restrict__ counter, float lr,
-                            float b1, float b2, float eps) {
+                            const float* __restrict__ pw, float lr, float b1, float b2,
+                            float eps) {
   const float b1p = pw[0], b2p = pw[1];
   const float alpha = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.f, b2p))),
                                 __fsub_rn(1.f, b1p));
@@ -262,23 +273,28 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
     v[i] = __fadd_rn(v[i], __fmul_rn(__fsub_rn(__fmul_rn(g[i], g[i]), v[i]), omb2));
     p[i] = __fsub_rn(p[i], __fdiv_rn(__fmul_rn(m[i], alpha), __fadd_rn(__fsqrt_rn(v[i]), eps)));
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned prev = atomicAdd(counter, 1u);
-    if (prev == gridDim.x - 1) {
-      pw[0] = __fmul_rn(b1p, b1);
-      pw[1] = __fmul_rn(b2p, b2);
-      atomicExch(counter, 0u);
-      __threadfence();
+}
+
+// AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2 (fp32),
+// for each network selected in mask (bit 0 actor, bit 1 critic).
+DDPG_DEV void advance_powers(float* pw, int mask, float b1, float b2) {
+  for (int net = 0; net < 2; ++net)
+    if (mask & (1 << net)) {
+      pw[2 * net] = __fmul_rn(pw[2 * net], b1);
+      pw[2 * net + 1] = __fmul_rn(pw[2 * net + 1], b2);
     }
-  }
+}
+
+__global__ void advance_powers_kernel(float* pw, int mask, float b1, float b2) {
+  advance_powers(pw, mask, b1, b2);
 }
 
 // ---------------------------------------------------------------- K7 soft update
 // networks.py:34-37: target.assign(theta * tau + target * (1. - tau)), fp32.
 __global__ void soft_update_kernel(const float* __restrict__ th, float* __restrict__ tt,
-                                   long long n, float tau, float omt) {
+                                   long long n, float tau, float omt, float* pw, int pw_mask,
+                                   float b1, float b2) {
+  if (pw_mask && blockIdx.x == 0 && threadIdx.x == 0) advance_powers(pw, pw_mask, b1, b2);
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
