@@ -33,12 +33,14 @@ PEAK_HBM_GBS = 8000.0           # 8 TB/s spec
 CONFIGS = {
     # name: (S, A, H1, H2, B per GPU, action_scale, label)
     "c3": (64, 16, 1024, 1024, 4096, 1.0,
-           "C3 synthetic S=64 A=16 actor/critic 1024/1024, batch 4096/GPU, fp32"),
+           "C3 synthetic S=64 A=16 actor/critic 1024/1024, batch 4096/GPU"),
     "c2": (4, 1, 128, 200, 64, 3.0,
-           "C2 InvertedPendulum-shaped S=4 A=1 128/200, batch 64, fp32"),
+           "C2 InvertedPendulum-shaped S=4 A=1 128/200, batch 64"),
     "c5": (376, 17, 2048, 2048, 4096, 1.0,
-           "C5 Humanoid-shaped S=376 A=17 2048/2048, batch 4096/GPU, fp32"),
+           "C5 Humanoid-shaped S=376 A=17 2048/2048, batch 4096/GPU"),
 }
+DEFAULT_DTYPE = {"c3": "fp32", "c2": "fp32", "c5": "bf16"}
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # ~2.5 PF dense (MI355X_MICROARCH.md)
 REPLAY_ROWS = 1_000_000
 
 
@@ -46,7 +48,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234):
+def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="fp32"):
     from distributed_ddpg_amd import networks as nets
     from distributed_ddpg_amd.learner import FusedLearner, fill_synthetic, init_comm
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
@@ -55,7 +57,7 @@ def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234):
     actor = nets.ActorNetwork(S, A, scale, 1e-4, 1e-3, None, h1=H1, h2=H2)
     critic = nets.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), None, h1=H1,
                                 h2=H2)
-    sess = nets.Session(device=device, batch_max=B, rank=rank, world=world)
+    sess = nets.Session(device=device, batch_max=B, rank=rank, world=world, dtype=dtype)
     actor.set_session(sess)
     critic.set_session(sess)
     sess.run(nets.global_variables_initializer(seed=seed))   # same init on every rank
@@ -181,6 +183,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-small", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=20)
+    ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
+                    help="GEMM operand precision (default: fp32, bf16 for c5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -196,8 +200,10 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     cfg = args.config
+    dtype = args.dtype or DEFAULT_DTYPE[cfg]
     S, A, H1, H2, B, scale, label = CONFIGS[cfg]
-    sess, rb, fl = build_learner(cfg, local, rank, world, args.replay)
+    label = "%s, %s GEMM operands (fp32 master weights/accumulation)" % (label, dtype)
+    sess, rb, fl = build_learner(cfg, local, rank, world, args.replay, dtype=dtype)
     el = timed(fl, sess, args.steps, args.warmup, world)
     ms = 1000.0 * el / args.steps
     value = world * args.steps / el   # batch-B updates processed by all ranks per second
@@ -210,9 +216,11 @@ def main():
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_flops = dom["flops"] / dom["launches"]
     achieved = dom_flops / (dom_avg_ms * 1e-3) / 1e12
+    peak = PEAK_BF16_MFMA_TFLOPS if dom_name.startswith("gemm_bf16") else PEAK_FP32_MFMA_TFLOPS
+    step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
-                "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
                 "avg_launch_us": round(dom_avg_ms * 1e3, 2),
                 "flop_per_launch": dom_flops, "launches_per_step":
                     dom["launches"] / args.profile_steps}
@@ -220,14 +228,14 @@ def main():
         "metric": "actor+critic updates/sec (batch %d per GPU, %d-wide MLPs)" % (B, H1),
         "value": round(value, 3), "unit": "updates/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "weak", "vs_baseline": None, "dtype": dtype,
         "data": "synthetic (replay ring of %d N(0,1)/U(-1,1)/Bernoulli(0.01) transitions; "
                 "random-init weights)" % args.replay,
         "config": {"workload": label, "state_dim": S, "action_dim": A, "hidden": [H1, H2],
                    "global_batch": B * world, "per_gpu_batch": B,
                    "parallelism": "dp%d" % world},
         "samples_per_s": round(value * B, 1),
-        "mfma_util_step": round(step_flops / (ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+        "mfma_util_step": round(step_flops / (ms * 1e-3) / 1e12 / step_peak, 4),
         "step_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
         "gemm_tflops": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else None,
         "gpu_busy_ms_per_step": round(gpu_ms, 4),

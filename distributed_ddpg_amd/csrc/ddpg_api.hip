@@ -15,8 +15,10 @@
 
 #include "../../include/ddpg_hip.h"
 #include "gemm_f32.h"
+#include "gemm_bf16.h"
 #include "kernels.h"
 #include "sampler.h"
+#include "small_batch.h"
 
 using namespace ddpg;
 
@@ -135,6 +137,12 @@ struct ddpg_ctx {
   int ldS, ldA, ldAH1, ldAH2, ldCH2, ldC;
   hipStream_t stream = nullptr;
   bool own_stream = true;
+  // launch target of the building blocks: == stream except inside the fused
+  // step, which forks independent branches onto aux[0..1] (fork/join events;
+  // captured into the step's hipGraph like any other dependency)
+  hipStream_t cur = nullptr;
+  hipStream_t aux[2] = {nullptr, nullptr};
+  hipEvent_t fj[8] = {};
   std::string err;
 
   // parameters (fp32 master) -- one allocation: theta|target|m|v|grad
@@ -154,6 +162,7 @@ struct ddpg_ctx {
   float *th1, *tcat, *ta2, *cat, *h, *dhp, *dcat;
   float *h1, *h2, *o, *mu, *cat2, *dhp2, *da, *dz3, *dz2, *dz1, *dain;
   float *ppart, *qpart, *colpart, *headpart;  // partial-sum scratch
+  float *ppart_t, *qpart_t;                   // target-path copies (concurrent branch)
   float *slab_W1, *slab_W2, *slab_W3, *slab_Ws, *slab_Wa, *slab_Wh;
   int split_cap_W1, split_cap_W2, split_cap_W3, split_cap_Ws, split_cap_Wa, split_cap_Wh;
   int* d_slots = nullptr;
@@ -174,6 +183,13 @@ struct ddpg_ctx {
   } gslot[2];
   int gcur = 0;
   bool use_graph = true;
+  bool par = false;  // env DDPG_PAR=1: fork independent branches onto aux streams
+  // small-batch fused path (small_batch.h): eligible dims, per-WG gradient slabs
+  bool sb_ok = false;
+  int sb_max_b = 0;
+  float* sb_part = nullptr;   // [ceil(sb_max_b / SB_R)][L.total]
+  float* sb_misc = nullptr;   // alpha[2] | stat_part[2 * G]
+  unsigned long long* sb_stamps = nullptr;  // diagnostic (DDPG_SB_STAMPS=1)
 
   // comm
   ncclComm_t comm = nullptr;
@@ -207,18 +223,19 @@ struct ProfScope {
   ProfScope(ddpg_ctx* ctx, const char* name, double flops, double bytes) : c(ctx) {
     if (!c->prof) return;
     ProfRec rec{name, ev_get(c), ev_get(c), flops, bytes};
-    HIP_TRY(hipEventRecord(rec.e0, c->stream));
+    HIP_TRY(hipEventRecord(rec.e0, c->cur));
     c->prof_recs.push_back(rec);
     idx = c->prof_recs.size() - 1;
   }
   ~ProfScope() {
-    if (idx != (size_t)-1) (void)hipEventRecord(c->prof_recs[idx].e1, c->stream);
+    if (idx != (size_t)-1) (void)hipEventRecord(c->prof_recs[idx].e1, c->cur);
   }
 };
 
 static void prof_collect(ddpg_ctx* c) {
   if (c->prof_recs.empty()) return;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto st : c->aux) HIP_TRY(hipStreamSynchronize(st));
   for (auto& r : c->prof_recs) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, r.e0, r.e1));
@@ -244,6 +261,7 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Block-count target for tile selection (env DDPG_GEMM_MIN_BLOCKS overrides).
 static int g_min_blocks = 1024;
+static int g_xcd_remap = 1;  // env DDPG_XCD=0 disables
 
 struct GemmPlan {
   int bm = 128, bn = 128, splits = 1, kps = 0;
@@ -278,9 +296,17 @@ static void pick_tile(int M, int N, int min_blocks, int* bm, int* bn) {
 
 // Plan for a plain (splits = 1) GEMM or a split-K weight-gradient GEMM
 // (splits = 0: auto, ~512 blocks, >= 128 k per split, <= cap).
-static GemmPlan make_plan(int M, int N, int K, int splits, int cap = 64) {
+static GemmPlan make_plan(int M, int N, int K, int splits, int cap = 64, bool big = false) {
   GemmPlan p;
-  if (splits == 1) {
+  if (big) {  // bf16 kernel: fixed 128 x 128 tile
+    p.bm = p.bn = 128;
+    if (splits != 1) {
+      const int tiles = ceil_div(M, 128) * ceil_div(N, 128);
+      splits = std::max(1, 512 / tiles);
+      splits = std::min(splits, std::max(1, K / 128));
+      splits = std::min(splits, cap);
+    }
+  } else if (splits == 1) {
     pick_tile(M, N, g_min_blocks, &p.bm, &p.bn);
   } else {
     p.bm = M <= 64 ? 64 : 128;
@@ -295,23 +321,31 @@ static GemmPlan make_plan(int M, int N, int K, int splits, int cap = 64) {
   return p;
 }
 
-template <int AL, int BL, int VEC>
+template <int AL, int BL, int VA, int VB>
 static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const GemmArgs& g) {
   if (p.bm == 128 && p.bn == 128)
-    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 128, 128>), grid, dim3(GNT), 0, st, g);
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VA, VB, 128, 128>), grid, dim3(GNT), 0, st, g);
   else if (p.bm == 128)
-    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 128, 64>), grid, dim3(GNT), 0, st, g);
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VA, VB, 128, 64>), grid, dim3(GNT), 0, st, g);
   else if (p.bn == 128)
-    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 64, 128>), grid, dim3(GNT), 0, st, g);
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VA, VB, 64, 128>), grid, dim3(GNT), 0, st, g);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VEC, 64, 64>), grid, dim3(GNT), 0, st, g);
+    hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VA, VB, 64, 64>), grid, dim3(GNT), 0, st, g);
 }
+
+static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec);
 
 template <int AL, int BL>
 static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
                             const float* B, int ldb, int M, int N, int K, const GemmEpi& e,
                             int splits = 1, int cap = 64) {
-  GemmPlan p = make_plan(M, N, K, splits, cap);
+  const int contA = (AL == L_RK) ? K : M;
+  const int contB = (BL == L_RK) ? K : N;
+  const bool va = (contA % 4 == 0) && (lda % 4 == 0) && aligned16(A);
+  const bool vb = (contB % 4 == 0) && (ldb % 4 == 0) && aligned16(B);
+  const bool vec = va && vb;
+  const bool bf = use_bf16(c, M, N, vec);
+  GemmPlan p = make_plan(M, N, K, splits, cap, bf);
   if (M <= 0 || N <= 0) return p;
   GemmArgs g;
   g.A = A;
@@ -322,24 +356,36 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   g.lda = lda;
   g.ldb = ldb;
   g.kps = p.kps;
+  g.xcd = g_xcd_remap;
   g.e = e;
-  const int contA = (AL == L_RK) ? K : M;
-  const int contB = (BL == L_RK) ? K : N;
-  const bool vec = (contA % 4 == 0) && (contB % 4 == 0) && (lda % 4 == 0) && (ldb % 4 == 0) &&
-                   aligned16(A) && aligned16(B);
   dim3 grid(p.nt(N), p.mt(M), p.splits);
   // profile key "<kernel symbol>|<phase>": the symbol part matches rocprofv3's kernel names
   static const char* lay[2] = {"RK", "KR"};
   char key[112];
-  snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d,%d,%d>|%s", lay[AL], lay[BL], vec ? 4 : 1,
-           p.bm, p.bn, name);
-  ProfScope ps(c, key, 2.0 * M * N * (double)K, 0.0);
-  if (vec)
-    gemm_dispatch<AL, BL, 4>(p, grid, c->stream, g);
+  if (bf)
+    snprintf(key, sizeof key, "gemm_bf16_kernel<%s,%s>|%s", lay[AL], lay[BL], name);
   else
-    gemm_dispatch<AL, BL, 1>(p, grid, c->stream, g);
+    snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d,%d,%d,%d>|%s", lay[AL], lay[BL],
+             va ? 4 : 1, vb ? 4 : 1, p.bm, p.bn, name);
+  ProfScope ps(c, key, 2.0 * M * N * (double)K, 0.0);
+  if (bf)
+    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), grid, dim3(GNT), 0, c->cur, g);
+  else if (va && vb)
+    gemm_dispatch<AL, BL, 4, 4>(p, grid, c->cur, g);
+  else if (va)
+    gemm_dispatch<AL, BL, 4, 1>(p, grid, c->cur, g);
+  else if (vb)
+    gemm_dispatch<AL, BL, 1, 4>(p, grid, c->cur, g);
+  else
+    gemm_dispatch<AL, BL, 1, 1>(p, grid, c->cur, g);
   HIP_TRY(hipGetLastError());
   return p;
+}
+
+// bf16 MFMA for the large GEMMs of a DDPG_BF16 context (thin / unaligned
+// shapes stay on the exact-fp32 kernel)
+static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec) {
+  return c->cfg.dtype == DDPG_BF16 && vec && M >= 128 && N >= 128;
 }
 
 // ====================================================================== building blocks
@@ -369,7 +415,7 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
   GemmPlan pl = gemm_launch<L_RK, L_KR>(c, "fwd_head", h1, c->ldAH1, P(c, base, L.a[AW2]),
                                         c->AH2, B, c->AH2, c->AH1, e);
   ProfScope ps(c, "actor_out", 0, 0);
-  hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
+  hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->cur,
                      c->ppart, pl.nt(c->AH2), B, c->A, c->cfg.action_scale, o, mu, c->ldA);
   HIP_TRY(hipGetLastError());
 }
@@ -433,7 +479,7 @@ static void critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int 
                                         P(c, c->theta, L.c[CWH]) + (size_t)c->CH1 * c->CH2,
                                         c->CH2, B, c->CH1, c->CH2, e);
   ProfScope ps(c, "action_grad", 0, 0);
-  hipLaunchKernelGGL(action_grad_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->stream,
+  hipLaunchKernelGGL(action_grad_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->cur,
                      c->ppart, pl.nt(c->CH1), B, c->A, B, o, c->ldA, c->cfg.action_scale, da,
                      dz3);
   HIP_TRY(hipGetLastError());
@@ -459,14 +505,14 @@ static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
   }
   ProfScope ps(c, name, 0, bytes);
   const int bx = (int)std::min<long long>(512, std::max<long long>(1, (maxc / 4 + 255) / 256));
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, tab.nseg), dim3(256), 0, c->stream, tab);
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, tab.nseg), dim3(256), 0, c->cur, tab);
   HIP_TRY(hipGetLastError());
 }
 
 static void allreduce(ddpg_ctx* c, float* buf, size_t n) {
   if (c->world <= 1 || !c->comm) return;
   ProfScope ps(c, "rccl_allreduce", 0, (double)n * 4.0);
-  ncclResult_t r = ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, c->comm, c->stream);
+  ncclResult_t r = ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, c->comm, c->cur);
   if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
 }
 
@@ -481,26 +527,37 @@ static void adam_launch(ddpg_ctx* c, int net, bool advance) {
   int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
   {
     ProfScope ps(c, "adam", 0, 28.0 * n);
-    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
                        c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net, lr,
                        c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon);
     HIP_TRY(hipGetLastError());
   }
   if (advance) {
-    hipLaunchKernelGGL(advance_powers_kernel, dim3(1), dim3(1), 0, c->stream, c->dpw, 1 << net,
+    hipLaunchKernelGGL(advance_powers_kernel, dim3(1), dim3(1), 0, c->cur, c->dpw, 1 << net,
                        c->cfg.beta1, c->cfg.beta2);
     HIP_TRY(hipGetLastError());
   }
 }
 
+// Fork/join between the ctx streams (par == false keeps everything on cur).
+static void fork_to(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
+  if (from == to) return;
+  HIP_TRY(hipEventRecord(c->fj[ev], from));
+  HIP_TRY(hipStreamWaitEvent(to, c->fj[ev], 0));
+}
+
 // Critic update on rows already in c->s / c->a with targets in c->y.
 // networks.py:130-137,170-175 (+ RCCL sum over ranks for world > 1).
-static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused) {
+// nq < 0: run the critic forward here; otherwise it already ran (fused step,
+// concurrently with the target path) and left nq Wo-projection slabs.
+// par: run dWh concurrently with dcat on aux[0].
+static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq = -1,
+                             bool par = false) {
   const Layout& L = c->L;
-  const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
+  if (nq < 0) nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
   {
     ProfScope ps(c, "critic_loss", 0, 0);
-    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->stream, c->qpart, nq, B,
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->cur, c->qpart, nq, B,
                        P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq, c->dstats, c->dacc);
     HIP_TRY(hipGetLastError());
   }
@@ -511,17 +568,23 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused) {
   {
     ProfScope ps(c, "critic_head_bwd", 0, (double)B * c->CH2 * 8.0);
     hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->CH2, 256), nchunk), dim3(256), 0,
-                       c->stream, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->CH2,
+                       c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->CH2,
                        kHeadRows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo);
     HIP_TRY(hipGetLastError());
   }
-  // dWh = cat^T . dh_pre   (split-K slabs)
+  // dWh = cat^T . dh_pre   (split-K slabs; on aux[0] when par)
+  const hipStream_t main = c->cur;
+  if (par) {
+    fork_to(c, 4, main, c->aux[0]);
+    c->cur = c->aux[0];
+  }
   GemmEpi e = epi_none();
   e.out = c->slab_Wh;
   e.ldo = c->CH2;
   e.out_split_stride = (long long)2 * c->CH1 * c->CH2;
   GemmPlan pWh = gemm_launch<L_KR, L_KR>(c, "wgrad", c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1,
                                          c->CH2, B, e, 0, c->split_cap_Wh);
+  c->cur = main;
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
   e = epi_none();
   e.post = 1;
@@ -545,6 +608,7 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused) {
   e.out_split_stride = (long long)c->A * c->CH1;
   GemmPlan pWa = gemm_launch<L_KR, L_KR>(c, "wgrad", c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A,
                                          c->CH1, B, e, 0, c->split_cap_Wa);
+  if (par) fork_to(c, 5, c->aux[0], main);  // join dWh
   // gather every critic gradient into the flat grad buffer
   float* G = c->grad;
   ReduceTable tab;
@@ -567,16 +631,23 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused) {
 
 // Actor update given dz3 (= TanhGrad chain of -dQ/da) and the forward
 // activations h1, h2 of c->s.  networks.py:39-47,71-75.
-static void actor_train_dev(ddpg_ctx* c, int B, bool fused) {
+// par: weight-gradient GEMMs (dW3, dW2) run on aux[0] beside the dX chain.
+static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   const Layout& L = c->L;
   float* G = c->grad;
+  const hipStream_t main = c->cur;
   // dW3 = h2^T . dz3
+  if (par) {
+    fork_to(c, 6, main, c->aux[0]);
+    c->cur = c->aux[0];
+  }
   GemmEpi e = epi_none();
   e.out = c->slab_W3;
   e.ldo = c->A;
   e.out_split_stride = (long long)c->AH2 * c->A;
   GemmPlan pW3 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A,
                                          B, e, 0, c->split_cap_W3);
+  c->cur = main;
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
   e = epi_none();
   e.post = 1;
@@ -589,13 +660,18 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused) {
   GemmPlan pz2 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A,
                                          B, c->AH2, c->A, e);
   const int mt2 = pz2.mt(B);
-  // dW2 = h1^T . dz2
+  // dW2 = h1^T . dz2   (aux[0] waits for dz2, then runs beside dz1)
+  if (par) {
+    fork_to(c, 7, main, c->aux[0]);
+    c->cur = c->aux[0];
+  }
   e = epi_none();
   e.out = c->slab_W2;
   e.ldo = c->AH2;
   e.out_split_stride = (long long)c->AH1 * c->AH2;
   GemmPlan pW2 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1,
                                          c->AH2, B, e, 0, c->split_cap_W2);
+  c->cur = main;
   // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
   float* colpart1 = c->colpart + (size_t)mt2 * c->AH2;
   e = epi_none();
@@ -615,6 +691,7 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused) {
   e.out_split_stride = (long long)c->S * c->AH1;
   GemmPlan pW1 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1,
                                          B, e, 0, c->split_cap_W1);
+  if (par) fork_to(c, 3, c->aux[0], main);  // join dW3, dW2
   ReduceTable tab;
   tab.nseg = 0;
   add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1, pW1.splits,
@@ -651,34 +728,161 @@ static void soft_update_dev(ddpg_ctx* c, int mask, int pw_mask) {
   const long long n = (long long)(e - b);
   int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
   ProfScope ps(c, "soft_update", 0, 12.0 * n);
-  hipLaunchKernelGGL(soft_update_kernel, dim3(blocks), dim3(256), 0, c->stream, c->theta + b,
+  hipLaunchKernelGGL(soft_update_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
                      c->target + b, n, tau, omt, c->dpw, pw_mask, c->cfg.beta1, c->cfg.beta2);
   HIP_TRY(hipGetLastError());
 }
 
 // One full learner step (ddpg.py:86-113) on rows already gathered into
 // c->s, c->a, c->r, c->t, c->s2 (B local rows, inv_b = 1/B_global).
+// Dependency-preserving concurrency (same results, bitwise): the target path
+// (aux[0]), the online actor forward (aux[1]) and the online critic forward
+// (main) are independent until the critic loss; inside the backward passes
+// the weight-gradient GEMMs run beside the dX chain.
 static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   const Layout& L = c->L;
+  const hipStream_t s0 = c->cur;
+  const hipStream_t s1 = c->par ? c->aux[0] : s0, s2 = c->par ? c->aux[1] : s0;
+  fork_to(c, 0, s0, s1);
+  fork_to(c, 0, s0, s2);
   // target_q = critic.predict_target(s2, actor.predict_target(s2))  ddpg.py:90
+  c->cur = s1;
+  std::swap(c->ppart, c->ppart_t);
+  std::swap(c->qpart, c->qpart_t);
   actor_fwd(c, c->target, c->s2, B, c->th1, nullptr, nullptr, c->ta2);
-  const int nq = critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr);
+  const int nqt = critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr);
   {
     ProfScope ps(c, "td_target", 0, 0);
-    hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->stream, c->qpart,
-                       nq, B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t, c->cfg.gamma,
+    hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->cur, c->qpart,
+                       nqt, B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t, c->cfg.gamma,
                        c->y);
     HIP_TRY(hipGetLastError());
   }
-  // critic.train(s, a, y)  ddpg.py:100
-  critic_train_dev(c, B, inv_b, true);
-  // a_outs = actor.predict(s); grads = critic.action_gradients(s, a_outs)  ddpg.py:106-107
+  std::swap(c->ppart, c->ppart_t);
+  std::swap(c->qpart, c->qpart_t);
+  // a_outs = actor.predict(s)  ddpg.py:106 (actor params are unchanged until actor.train)
+  c->cur = s2;
   actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu);
+  // critic.train(s, a, y)  ddpg.py:100: forward now, loss once y is ready
+  c->cur = s0;
+  const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
+  fork_to(c, 1, s1, s0);  // join target path (y)
+  critic_train_dev(c, B, inv_b, true, nq, c->par);
+  // grads = critic.action_gradients(s, a_outs)  ddpg.py:107 (updated critic)
+  fork_to(c, 2, s2, s0);  // join online actor forward (h1, h2, o, mu)
   critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);
   // actor.train(s, grads[0])  ddpg.py:109  (forward above reused: same params)
-  actor_train_dev(c, B, true);
+  actor_train_dev(c, B, true, c->par);
   // actor/critic.update_target_network()  ddpg.py:112-113 (+ both Adam power updates)
   soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC, 3);
+}
+
+// Small-batch learner step: 4 launches (small_batch.h).  Rows already
+// gathered into c->s, c->a, c->r, c->t, c->s2.
+static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
+  const Layout& L = c->L;
+  SbArgs a;
+  memset(&a, 0, sizeof a);
+  a.B = B;
+  a.S = c->S;
+  a.A = c->A;
+  a.AH1 = c->AH1;
+  a.AH2 = c->AH2;
+  a.CH1 = c->CH1;
+  a.CH2 = c->CH2;
+  a.ldS = c->ldS;
+  a.ldA = c->ldA;
+  a.LX = rup(std::max(c->S, c->A), 4);
+  a.LA = rup(std::max(c->AH1, 2 * c->CH1), 4);
+  a.LB = rup(std::max(c->AH2, c->CH2), 4);
+  a.LC = rup(2 * c->CH1, 4);
+  a.LD = rup(std::max(c->CH2, c->AH2), 4);
+  a.inv_b = inv_b;
+  a.gamma = c->cfg.gamma;
+  a.scale = c->cfg.action_scale;
+  a.tau = c->cfg.tau;
+  a.omt = (float)(1.0 - (double)c->cfg.tau);
+  a.b1 = c->cfg.beta1;
+  a.b2 = c->cfg.beta2;
+  a.lr_a = c->cfg.actor_lr;
+  a.lr_c = c->cfg.critic_lr;
+  a.eps = c->cfg.epsilon;
+  a.s = c->s;
+  a.s2 = c->s2;
+  a.a = c->a;
+  a.r = c->r;
+  a.t = c->t;
+  a.theta = c->theta;
+  a.target = c->target;
+  a.adam_m = c->adam_m;
+  a.adam_v = c->adam_v;
+  a.part = c->sb_part;
+  a.PT = (long long)L.total;
+  a.pw = c->dpw;
+  a.alpha = c->sb_misc;
+  a.stat_part = c->sb_misc + 4;
+  a.stats = c->dstats;
+  a.acc = c->dacc;
+  a.stamps = c->sb_stamps;
+  a.aW1 = L.a[AW1].off;
+  a.ab1 = L.a[AB1].off;
+  a.aW2 = L.a[AW2].off;
+  a.ab2 = L.a[AB2].off;
+  a.aW3 = L.a[AW3].off;
+  a.cWs = L.c[CWS].off;
+  a.cbs = L.c[CBS].off;
+  a.cWa = L.c[CWA].off;
+  a.cba = L.c[CBA].off;
+  a.cWh = L.c[CWH].off;
+  a.cbh = L.c[CBH].off;
+  a.cWo = L.c[CWO].off;
+  a.cbo = L.c[CBO].off;
+  a.actor_begin = L.actor_begin;
+  a.actor_end = L.actor_end;
+  a.critic_begin = L.critic_begin;
+  a.critic_end = L.critic_end;
+  const int G = ceil_div(B, SB_R);
+  const size_t smem = ((size_t)SB_R * (4 * a.LX + a.LA + a.LB + a.LC + a.LD + 8) +
+                       (SB_NT / 64) * SB_R * SB_NMAX) * sizeof(float);
+  const long long nc = (long long)(L.critic_end - L.critic_begin);
+  const long long na = (long long)(L.actor_end - L.actor_begin);
+  const int bc = (int)std::min<long long>(1024, (nc + 255) / 256);
+  const int ba = (int)std::min<long long>(1024, (na + 255) / 256);
+  {
+    ProfScope ps(c, "sb_phase1", 0, 0);
+    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
+    HIP_TRY(hipGetLastError());
+  }
+  if (c->sb_stamps && getenv("DDPG_SB_TWICE")) {  // diagnostic: warm re-run (perturbs pw)
+    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
+    HIP_TRY(hipGetLastError());
+  }
+  {
+    ProfScope ps(c, "sb_reduce_adam", 0, (double)nc * 4.0 * (G + 7));
+    hipLaunchKernelGGL(sb_reduce_adam_kernel, dim3(bc), dim3(256), 0, c->cur, a, 1, G);
+    HIP_TRY(hipGetLastError());
+  }
+  {
+    ProfScope ps(c, "sb_phase3", 0, 0);
+    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
+    HIP_TRY(hipGetLastError());
+  }
+  if (c->sb_stamps && getenv("DDPG_SB_TWICE")) {
+    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
+    HIP_TRY(hipGetLastError());
+  }
+  {
+    ProfScope ps(c, "sb_reduce_adam", 0, (double)na * 4.0 * (G + 7));
+    hipLaunchKernelGGL(sb_reduce_adam_kernel, dim3(ba), dim3(256), 0, c->cur, a, 0, G);
+    HIP_TRY(hipGetLastError());
+  }
+}
+
+static void learner_step_any(ddpg_ctx* c, int B, float inv_b) {
+  if (c->sb_ok && c->world == 1 && B <= c->sb_max_b)
+    learner_step_small(c, B, inv_b);
+  else
+    learner_step_dev(c, B, inv_b);
 }
 
 // ====================================================================== helpers
@@ -737,9 +941,15 @@ static void ctx_free(ddpg_ctx* c) {
     if (g.h_idx) (void)hipHostFree(g.h_idx);
     if (g.done) (void)hipEventDestroy(g.done);
   }
+  for (void* p : {(void*)c->sb_part, (void*)c->sb_misc, (void*)c->sb_stamps})
+    if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc})
     if (p) (void)hipFree(p);
+  for (auto st : c->aux)
+    if (st) (void)hipStreamDestroy(st);
+  for (auto ev : c->fj)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -781,7 +991,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       throw einval("dims must be positive (S=%d A=%d H1=%d H2=%d Bmax=%d)", k.state_dim,
                    k.action_dim, k.h1, k.h2, k.batch_max);
     if (k.action_dim > PROJ_MAX) throw einval("action_dim %d > %d", k.action_dim, PROJ_MAX);
-    if (k.dtype != DDPG_FP32) throw einval("dtype %d not supported by this build", k.dtype);
+    if (k.dtype != DDPG_FP32 && k.dtype != DDPG_BF16) throw einval("bad dtype %d", k.dtype);
     c->cfg = k;
     c->S = k.state_dim;
     c->A = k.action_dim;
@@ -801,6 +1011,9 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     c->L.build(c->S, c->A, c->AH1, c->AH2, c->CH1, c->CH2);
     HIP_TRY(hipSetDevice(k.device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->cur = c->stream;
+    for (auto& st : c->aux) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (auto& ev : c->fj) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const size_t PT = c->L.total;
     HIP_TRY(hipMalloc(&c->dparams, 5 * PT * sizeof(float)));
     HIP_TRY(hipMemset(c->dparams, 0, 5 * PT * sizeof(float)));
@@ -826,6 +1039,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     const int mt = ceil_div(c->Bmax, 64);
     const int nchunk = ceil_div(c->Bmax, kHeadRows);
     if (const char* mb = getenv("DDPG_GEMM_MIN_BLOCKS")) g_min_blocks = std::max(1, atoi(mb));
+    if (const char* xv = getenv("DDPG_XCD")) g_xcd_remap = atoi(xv) != 0;
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;
     c->split_cap_W3 = make_plan(c->AH2, c->A, c->Bmax, 0).splits;
@@ -848,6 +1062,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
         {&c->dz1, B * c->ldAH1}, {&c->dain, B * c->A},
         {&c->ppart, (size_t)NTP * B * PROJ_MAX},
         {&c->qpart, (size_t)NTQ * B},
+        {&c->ppart_t, (size_t)NTP * B * PROJ_MAX},
+        {&c->qpart_t, (size_t)NTQ * B},
         {&c->colpart, (size_t)mt * std::max(2 * c->CH1, c->AH2 + c->AH1)},
         {&c->headpart, (size_t)nchunk * (2 * c->CH2 + 1)},
         {&c->slab_W1, (size_t)c->split_cap_W1 * c->S * c->AH1},
@@ -875,6 +1091,26 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
     }
     if (const char* gv = getenv("DDPG_GRAPH")) c->use_graph = atoi(gv) != 0;
+    if (const char* pv = getenv("DDPG_PAR")) c->par = atoi(pv) != 0;
+    {
+      const int hmax = std::max(std::max(c->AH1, c->AH2), std::max(c->CH1, c->CH2));
+      bool ok = c->world == 1 && hmax <= 512 && (c->CH1 % 4) == 0;
+      if (const char* sv = getenv("DDPG_SMALL")) ok = ok && atoi(sv) != 0;
+      if (ok) {
+        c->sb_max_b = std::min(c->Bmax, 512);
+        const int G = ceil_div(c->sb_max_b, SB_R);
+        HIP_TRY(hipMalloc(&c->sb_part, (size_t)G * c->L.total * sizeof(float)));
+        HIP_TRY(hipMemset(c->sb_part, 0, (size_t)G * c->L.total * sizeof(float)));
+        HIP_TRY(hipMalloc(&c->sb_misc, (4 + 2 * (size_t)G) * sizeof(float)));
+        HIP_TRY(hipMemset(c->sb_misc, 0, (4 + 2 * (size_t)G) * sizeof(float)));
+        c->sb_ok = true;
+        if (const char* st = getenv("DDPG_SB_STAMPS"))
+          if (atoi(st)) {
+            HIP_TRY(hipMalloc(&c->sb_stamps, 16 * sizeof(unsigned long long)));
+            HIP_TRY(hipMemset(c->sb_stamps, 0, 16 * sizeof(unsigned long long)));
+          }
+      }
+    }
     HIP_TRY(hipDeviceSynchronize());
   });
   if (rc != DDPG_OK) {
@@ -894,7 +1130,26 @@ void ddpg_destroy(ddpg_ctx* c) {
 }
 
 int ddpg_sync(ddpg_ctx* c) {
-  return guard(c, [&] { HIP_TRY(hipStreamSynchronize(c->stream)); });
+  return guard(c, [&] {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->sb_stamps) {  // diagnostic: section cycle counts of the last small-batch step
+      unsigned long long t[16];
+      HIP_TRY(hipMemcpy(t, c->sb_stamps, sizeof t, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[sb stamps] phase1:");
+      unsigned long long prev = t[15];
+      for (int i = 0; i <= 5; ++i) {
+        fprintf(stderr, " %llu", t[i] - prev);
+        prev = t[i];
+      }
+      fprintf(stderr, " | phase3:");
+      prev = t[14];
+      for (int i = 8; i <= 13; ++i) {
+        fprintf(stderr, " %llu", t[i] - prev);
+        prev = t[i];
+      }
+      fprintf(stderr, "\n");
+    }
+  });
 }
 
 int ddpg_set_stream(ddpg_ctx* c, void* s) {
@@ -908,6 +1163,7 @@ int ddpg_set_stream(ddpg_ctx* c, void* s) {
       HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       c->own_stream = true;
     }
+    c->cur = c->stream;
   });
 }
 
@@ -1314,7 +1570,7 @@ int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* 
 // ---------------------------------------------------------------- fused step
 static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
   ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->stream,
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->cur,
                      c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, c->S, c->A, c->s,
                      c->s2, c->ldS, c->a, c->ldA, c->r, c->t, c->has_scaler ? c->dmean : nullptr,
                      c->has_scaler ? c->dscale : nullptr);
@@ -1346,7 +1602,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
         HIP_TRY(hipMemcpyAsync(c->d_slots, g.h_idx, (size_t)B * sizeof(int),
                                hipMemcpyHostToDevice, c->stream));
         gather_launch(c, rb, B);
-        learner_step_dev(c, B, inv_b);
+        learner_step_any(c, B, inv_b);
       } catch (...) {
         (void)hipStreamEndCapture(c->stream, &graph);
         throw;
@@ -1370,7 +1626,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
                            c->stream));
     HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
     gather_launch(c, rb, B);
-    learner_step_dev(c, B, inv_b);
+    learner_step_any(c, B, inv_b);
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
   if (stats) {

@@ -386,3 +386,103 @@ def test_graph_replay_matches_eager(dd, O, monkeypatch):
     for x, y in zip(p1, p0):
         for u, v in zip(x, y):
             assert np.array_equal(u, v)
+
+
+# ---------------------------------------------------------------------- bf16
+# bf16 GEMM operands (v_mfma_f32_32x32x16_bf16), fp32 accumulation, fp32
+# master weights / Adam / epilogues.  Stated bf16 tolerances (vs the fp64
+# oracle, max-rel per tensor): forward outputs 2e-2; dQ/da 5e-2; parameters
+# after 3 fused steps 2e-2 (Adam moves every weight by ~lr per step, so the
+# parameter error stays a fraction of lr even with bf16 gradients).
+BF16_FWD_TOL, BF16_DA_TOL, BF16_PARAM_TOL = 2e-2, 5e-2, 2e-2
+
+
+def _session_dtype(dd, O, name, p, dtype, batch_max=4096):
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    from distributed_ddpg_amd import _lib
+    dd.reset_default_graph()
+    actor = dd.ActorNetwork(S, A, scale, 1e-4, 1e-3, None, h1=H1, h2=H2)
+    critic = dd.CriticNetwork(S, A, 1e-3, 1e-3, 10, None, h1=H1, h2=H2)
+    sess = dd.Session(batch_max=batch_max, dtype=dtype)
+    actor.set_session(sess)
+    critic.set_session(sess)
+    sess.set_params(_lib.ACTOR, [p["actor"][k] for k in O.ACTOR_KEYS])
+    sess.set_params(_lib.ACTOR_TARGET, [p["actor_t"][k] for k in O.ACTOR_KEYS])
+    sess.set_params(_lib.CRITIC, [p["critic"][k] for k in O.CRITIC_KEYS])
+    sess.set_params(_lib.CRITIC_TARGET, [p["critic_t"][k] for k in O.CRITIC_KEYS])
+    return sess, actor, critic
+
+
+def test_bf16_parity_and_kernel_use(dd, O):
+    import random
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS["wide"]
+    p, _ = _params(O, "wide")
+    sess, actor, critic = _session_dtype(dd, O, "wide", p, "bf16")
+    s, a, _ = _batch("wide", seed=21)
+    mu = actor.predict(s)
+    assert rel(mu, O.actor_forward(f64(p["actor"]), s.astype(np.float64), scale)[3]) < BF16_FWD_TOL
+    q = critic.predict(s, a)
+    assert rel(q, O.critic_forward(f64(p["critic"]), s.astype(np.float64),
+                                   a.astype(np.float64))[3]) < BF16_FWD_TOL
+    (da,) = critic.action_gradients(s, mu)
+    assert rel(da, O.critic_action_grads(f64(p["critic"]), s.astype(np.float64),
+                                         mu.astype(np.float64))) < BF16_DA_TOL
+    rb = ReplayBuffer(5000, 1234)
+    rows = _fill(rb, S, A, 3000, scale, seed=2)
+    fl = FusedLearner(sess, rb, B)
+    prof = Profile(sess)
+    prof.enable(True)
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    ref_rng = random.Random(1234)
+    for it in range(3):
+        idx = np.array(ref_rng.sample(range(3000), B))
+        fl.step()
+        L.step(*(x[idx] for x in rows))
+    keys = prof.read()
+    prof.enable(False)
+    assert any(k.startswith("gemm_bf16_kernel") for k in keys), sorted(keys)
+    for which, net, names in ((_lib.ACTOR, "actor", O.ACTOR_KEYS),
+                              (_lib.CRITIC, "critic", O.CRITIC_KEYS)):
+        for k, v in zip(names, sess.get_params(which)):
+            assert rel(v, L.state()[net][k].reshape(v.shape)) < BF16_PARAM_TOL, (net, k)
+    sess.close()
+
+
+@pytest.mark.parametrize("name", ["ip", "odd"])
+def test_small_batch_path_matches_large_path(dd, O, monkeypatch, name):
+    """The fused small-batch path (small_batch.h, 4 launches) and the
+    large-batch GEMM path (DDPG_SMALL=0) agree after 4 steps (different
+    summation order only), and both track the oracle."""
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    res = {}
+    for small in ("1", "0"):
+        monkeypatch.setenv("DDPG_SMALL", small)
+        sess, actor, critic = _session(dd, O, name, p)
+        rb = ReplayBuffer(4000, 5)
+        _fill(rb, S, A, 3000, scale, seed=8)
+        fl = FusedLearner(sess, rb, B)
+        prof = Profile(sess)
+        prof.enable(True)
+        st = [fl.step(stats=True) for _ in range(4)]
+        keys = prof.read()
+        prof.enable(False)
+        assert any(k.startswith("sb_phase") for k in keys) == (small == "1"), sorted(keys)
+        res[small] = (st, [sess.get_params(w) for w in (_lib.ACTOR, _lib.CRITIC,
+                                                       _lib.ACTOR_TARGET, _lib.CRITIC_TARGET)],
+                      sess.get_adam_powers(0), sess.get_adam_powers(1))
+        sess.close()
+    (s1, p1, a1, c1), (s0, p0, a0, c0) = res["1"], res["0"]
+    assert a1 == a0 and c1 == c0
+    for (q1, l1), (q0, l0) in zip(s1, s0):
+        assert abs(q1 - q0) <= 1e-5 * max(1.0, abs(q0))
+        assert abs(l1 - l0) <= 1e-4 * abs(l0)
+    for x, y in zip(p1, p0):
+        for u, v in zip(x, y):
+            assert rel(u, v) < GRAD_TOL
