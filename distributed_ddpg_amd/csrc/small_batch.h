@@ -289,6 +289,9 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   sb_load_rows(xs, g.LX, g.s, g.ldS, g.S, r0, valid);
   sb_load_rows(xs2, g.LX, g.s2, g.ldS, g.S, r0, valid);
   sb_load_rows(xa, g.LX, g.a, g.ldA, g.A, r0, valid);
+  // ta2 is written only in its first A columns; the padding up to LX feeds
+  // the next layer's zero-padded k group and must be 0, not stale LDS
+  for (int idx = tid; idx < SB_R * g.LX; idx += SB_NT) ta2[idx] = 0.f;
   __syncthreads();
   SB_STAMP(0);
   // ---- target actor: ta2 = scale * tanh(elu(elu(s2 W1 + b1) W2 + b2) W3)
@@ -392,6 +395,8 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   if (g.stamps && blockIdx.x == 0 && tid == 0) g.stamps[14] = __builtin_amdgcn_s_memtime();
   if (blockIdx.x == 0 && tid == 0) sb_alpha_and_advance(g.pw, g.alpha, g.lr_a, g.b1, g.b2);
   sb_load_rows(xs, g.LX, g.s, g.ldS, g.S, r0, valid);
+  // o / mu / dz3 are written only in their first A columns (see phase 1)
+  for (int idx = tid; idx < 3 * SB_R * g.LX; idx += SB_NT) o[idx] = 0.f;
   __syncthreads();
   SB_STAMP(8);
   // ---- online actor forward (current actor params): h1 -> bufA, h2 -> bufB, o, mu
