@@ -127,6 +127,23 @@ def summarize_profile(rows, steps):
     return by_kernel, dom, gpu_ms, gemm_ms, gemm_flops
 
 
+def pmc_traffic(cfg_name, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_<config>.json, written by profiles/pmc_traffic.py from a
+    FETCH_SIZE pass and a WRITE_SIZE pass of this same bench command, with the
+    gfx950 FETCH_SIZE x2 correction).  PMC counters cannot be read in-process."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % cfg_name)))
+    for fn in reversed(files):
+        try:
+            k = json.load(open(fn))["kernels"].get(kernel)
+        except (OSError, ValueError):
+            continue
+        if k:
+            return round(k["traffic_bytes_per_launch"]), os.path.relpath(fn, ROOT)
+    return None, None
+
+
 def cpu_baseline(cfg_name, budget_s=12.0):
     """Oracle (numpy fp32, TF op sequence incl. actor-forward recompute) on
     the host cores; a bounded sample of learner steps at the same config."""
@@ -218,9 +235,12 @@ def main():
     achieved = dom_flops / (dom_avg_ms * 1e-3) / 1e12
     peak = PEAK_BF16_MFMA_TFLOPS if dom_name.startswith("gemm_bf16") else PEAK_FP32_MFMA_TFLOPS
     step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    traffic, traffic_src = pmc_traffic(cfg, dom_name)
     roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
                 "avg_launch_us": round(dom_avg_ms * 1e3, 2),
                 "flop_per_launch": dom_flops, "launches_per_step":
                     dom["launches"] / args.profile_steps}

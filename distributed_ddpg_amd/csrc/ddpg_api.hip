@@ -367,7 +367,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   else
     snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d,%d,%d,%d>|%s", lay[AL], lay[BL],
              va ? 4 : 1, vb ? 4 : 1, p.bm, p.bn, name);
-  ProfScope ps(c, key, 2.0 * M * N * (double)K, 0.0);
+  // algorithmic bytes: each operand read once, the output (per split slab) written once
+  ProfScope ps(c, key, 2.0 * M * N * (double)K,
+               4.0 * ((double)M * K + (double)K * N + (double)M * N * p.splits));
   if (bf)
     hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), grid, dim3(GNT), 0, c->cur, g);
   else if (va && vb)

@@ -1,0 +1,67 @@
+"""Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+  python profiles/pmc_traffic.py <fetch_dir> <write_dir> <config> > profiles/rN_pmc_<config>.json
+
+Each pass is its own run of the same bench command (FETCH_SIZE takes 3 of the 4
+TCC slots, WRITE_SIZE 2, so they cannot share one pass), e.g.
+
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+      -d gpurun_out/pmc_fetch -o run -- python3 bench.py --no-cpu --no-small ...
+
+Corrections (MI355X_MICROARCH.md, HBM section): rocprofv3 reports both counters in
+KB; on gfx950 FETCH_SIZE counts 128-B requests at 64 B, i.e. exactly half the bytes
+of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact for
+16-B-per-lane streaming stores.  Infinity-Cache hits are counted as fetches.
+bench.py reads the JSON this writes and reports traffic = corrected fetch + write
+bytes per launch of the dominant kernel.
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+
+def bench_name(rocprof_name):
+    """'void ddpg::gemm_f32_kernel<0, 1, 4, 4, 64, 64>(ddpg::GemmArgs)' -> bench key."""
+    m = re.search(r"ddpg::(\w+)(?:<([^>]*)>)?\(", rocprof_name)
+    if not m:
+        return rocprof_name
+    sym, targs = m.group(1), m.group(2)
+    if targs is None:
+        return sym
+    a = [x.strip() for x in targs.split(",")]
+    lay = {"0": "RK", "1": "KR"}
+    a[0], a[1] = lay.get(a[0], a[0]), lay.get(a[1], a[1])
+    return "%s<%s>" % (sym, ",".join(a))
+
+
+def load(path, counter):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
+        if r["Counter_Name"] == counter:
+            agg[bench_name(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+    return agg
+
+
+def main(fetch_dir, write_dir, config):
+    f, w = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
+    out = {"config": config, "source": [fetch_dir, write_dir],
+           "correction": "fetch_bytes = 2 x FETCH_SIZE (gfx950 half-count of 128-B requests); "
+                         "write_bytes = WRITE_SIZE; KB -> B x 1024",
+           "kernels": {}}
+    for k in sorted(set(f) | set(w)):
+        fb = sum(f.get(k, [0.0])) / max(1, len(f.get(k, [])))
+        wb = sum(w.get(k, [0.0])) / max(1, len(w.get(k, [])))
+        out["kernels"][k] = {"launches": len(f.get(k, [])),
+                             "fetch_size_raw_per_launch": fb,
+                             "fetch_bytes_per_launch": 2.0 * fb,
+                             "write_bytes_per_launch": wb,
+                             "traffic_bytes_per_launch": 2.0 * fb + wb}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
