@@ -189,7 +189,10 @@ struct ddpg_ctx {
   int sb_max_b = 0;
   float* sb_part = nullptr;   // [ceil(sb_max_b / SB_R)][L.total]
   float* sb_misc = nullptr;   // alpha[2] | stat_part[2 * G]
-  unsigned long long* sb_stamps = nullptr;  // diagnostic (DDPG_SB_STAMPS=1)
+  float* sb_whT = nullptr;    // [CH2][2 CH1] critic Wh^T shadow
+  float* sb_w2T = nullptr;    // [AH2][AH1]   actor W2^T shadow
+  bool sb_shadow_ok = false;  // cleared by every theta write outside the small path
+  size_t sb_smem = 0;         // dynamic LDS bytes of the phase kernels
 
   // comm
   ncclComm_t comm = nullptr;
@@ -527,6 +530,7 @@ static void adam_launch(ddpg_ctx* c, int net, bool advance) {
   const long long n = (long long)(e - b);
   const float lr = net == 0 ? c->cfg.actor_lr : c->cfg.critic_lr;
   int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
+  c->sb_shadow_ok = false;
   {
     ProfScope ps(c, "adam", 0, 28.0 * n);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
@@ -779,10 +783,18 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC, 3);
 }
 
-// Small-batch learner step: 4 launches (small_batch.h).  Rows already
-// gathered into c->s, c->a, c->r, c->t, c->s2.
-static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
+// Small-batch learner step: 4 launches (small_batch.h); the gather from the
+// replay ring is fused into the phase kernels (slots already in c->d_slots).
+static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   const Layout& L = c->L;
+  if (!c->sb_shadow_ok) {  // a parameter write outside this path: rebuild the W^T shadows
+    hipLaunchKernelGGL(sb_transpose_kernel, dim3(64), dim3(256), 0, c->cur,
+                       c->theta + L.c[CWH].off, 2 * c->CH1, c->CH2, c->sb_whT);
+    hipLaunchKernelGGL(sb_transpose_kernel, dim3(64), dim3(256), 0, c->cur,
+                       c->theta + L.a[AW2].off, c->AH1, c->AH2, c->sb_w2T);
+    HIP_TRY(hipGetLastError());
+    c->sb_shadow_ok = true;
+  }
   SbArgs a;
   memset(&a, 0, sizeof a);
   a.B = B;
@@ -792,8 +804,6 @@ static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
   a.AH2 = c->AH2;
   a.CH1 = c->CH1;
   a.CH2 = c->CH2;
-  a.ldS = c->ldS;
-  a.ldA = c->ldA;
   a.LX = rup(std::max(c->S, c->A), 4);
   a.LA = rup(std::max(c->AH1, 2 * c->CH1), 4);
   a.LB = rup(std::max(c->AH2, c->CH2), 4);
@@ -809,15 +819,20 @@ static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
   a.lr_a = c->cfg.actor_lr;
   a.lr_c = c->cfg.critic_lr;
   a.eps = c->cfg.epsilon;
-  a.s = c->s;
-  a.s2 = c->s2;
-  a.a = c->a;
-  a.r = c->r;
-  a.t = c->t;
+  a.slots = c->d_slots;
+  a.rs = rb->rs;
+  a.ra = rb->ra;
+  a.rr = rb->rr;
+  a.rt = rb->rt;
+  a.rs2 = rb->rs2;
+  a.mean = c->has_scaler ? c->dmean : nullptr;
+  a.sdev = c->has_scaler ? c->dscale : nullptr;
   a.theta = c->theta;
   a.target = c->target;
   a.adam_m = c->adam_m;
   a.adam_v = c->adam_v;
+  a.whT = c->sb_whT;
+  a.w2T = c->sb_w2T;
   a.part = c->sb_part;
   a.PT = (long long)L.total;
   a.pw = c->dpw;
@@ -825,7 +840,6 @@ static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
   a.stat_part = c->sb_misc + 4;
   a.stats = c->dstats;
   a.acc = c->dacc;
-  a.stamps = c->sb_stamps;
   a.aW1 = L.a[AW1].off;
   a.ab1 = L.a[AB1].off;
   a.aW2 = L.a[AW2].off;
@@ -844,19 +858,14 @@ static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
   a.critic_begin = L.critic_begin;
   a.critic_end = L.critic_end;
   const int G = ceil_div(B, SB_R);
-  const size_t smem = ((size_t)SB_R * (4 * a.LX + a.LA + a.LB + a.LC + a.LD + 8) +
-                       (SB_NT / 64) * SB_R * SB_NMAX) * sizeof(float);
   const long long nc = (long long)(L.critic_end - L.critic_begin);
   const long long na = (long long)(L.actor_end - L.actor_begin);
   const int bc = (int)std::min<long long>(1024, (nc + 255) / 256);
   const int ba = (int)std::min<long long>(1024, (na + 255) / 256);
+  const double row_bytes = (2.0 * c->S + c->A + 2) * 4.0;
   {
-    ProfScope ps(c, "sb_phase1", 0, 0);
-    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
-    HIP_TRY(hipGetLastError());
-  }
-  if (c->sb_stamps && getenv("DDPG_SB_TWICE")) {  // diagnostic: warm re-run (perturbs pw)
-    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
+    ProfScope ps(c, "sb_phase1", 0, 4.0 * (double)G * (L.total + nc) + B * row_bytes);
+    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
   {
@@ -865,12 +874,8 @@ static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
     HIP_TRY(hipGetLastError());
   }
   {
-    ProfScope ps(c, "sb_phase3", 0, 0);
-    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
-    HIP_TRY(hipGetLastError());
-  }
-  if (c->sb_stamps && getenv("DDPG_SB_TWICE")) {
-    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G), dim3(SB_NT), smem, c->cur, a);
+    ProfScope ps(c, "sb_phase3", 0, 4.0 * (double)G * (L.total + na) + B * c->S * 4.0);
+    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
   {
@@ -880,11 +885,17 @@ static void learner_step_small(ddpg_ctx* c, int B, float inv_b) {
   }
 }
 
-static void learner_step_any(ddpg_ctx* c, int B, float inv_b) {
-  if (c->sb_ok && c->world == 1 && B <= c->sb_max_b)
-    learner_step_small(c, B, inv_b);
-  else
+static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B);
+
+// The fused learner step on this step's slots (c->d_slots): the small-batch
+// path (gather fused) or gather + the large-batch GEMM path.
+static void learner_step_any(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
+  if (c->sb_ok && c->world == 1 && B <= c->sb_max_b) {
+    learner_step_small(c, rb, B, inv_b);
+  } else {
+    gather_launch(c, rb, B);
     learner_step_dev(c, B, inv_b);
+  }
 }
 
 // ====================================================================== helpers
@@ -943,7 +954,7 @@ static void ctx_free(ddpg_ctx* c) {
     if (g.h_idx) (void)hipHostFree(g.h_idx);
     if (g.done) (void)hipEventDestroy(g.done);
   }
-  for (void* p : {(void*)c->sb_part, (void*)c->sb_misc, (void*)c->sb_stamps})
+  for (void* p : {(void*)c->sb_part, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc})
@@ -1096,21 +1107,29 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     if (const char* pv = getenv("DDPG_PAR")) c->par = atoi(pv) != 0;
     {
       const int hmax = std::max(std::max(c->AH1, c->AH2), std::max(c->CH1, c->CH2));
-      bool ok = c->world == 1 && hmax <= 512 && (c->CH1 % 4) == 0;
+      const int LX = rup(std::max(c->S, c->A), 4), LA = rup(std::max(c->AH1, 2 * c->CH1), 4);
+      const int LB = rup(std::max(c->AH2, c->CH2), 4), LC = rup(2 * c->CH1, 4);
+      const int LD = rup(std::max(c->CH2, c->AH2), 4);
+      const size_t smem = sb_smem_floats(LX, LA, LB, LC, LD) * sizeof(float);
+      // vector weight streams need 4-aligned widths; 160 KiB of LDS per workgroup
+      bool ok = c->world == 1 && hmax <= SB_MAXH && c->AH1 % 4 == 0 && c->AH2 % 4 == 0 &&
+                c->CH1 % 4 == 0 && c->CH2 % 4 == 0 && smem <= 160 * 1024;
       if (const char* sv = getenv("DDPG_SMALL")) ok = ok && atoi(sv) != 0;
       if (ok) {
         c->sb_max_b = std::min(c->Bmax, 512);
+        c->sb_smem = smem;
         const int G = ceil_div(c->sb_max_b, SB_R);
         HIP_TRY(hipMalloc(&c->sb_part, (size_t)G * c->L.total * sizeof(float)));
         HIP_TRY(hipMemset(c->sb_part, 0, (size_t)G * c->L.total * sizeof(float)));
         HIP_TRY(hipMalloc(&c->sb_misc, (4 + 2 * (size_t)G) * sizeof(float)));
         HIP_TRY(hipMemset(c->sb_misc, 0, (4 + 2 * (size_t)G) * sizeof(float)));
+        HIP_TRY(hipMalloc(&c->sb_whT, (size_t)2 * c->CH1 * c->CH2 * sizeof(float)));
+        HIP_TRY(hipMalloc(&c->sb_w2T, (size_t)c->AH1 * c->AH2 * sizeof(float)));
+        HIP_TRY(hipFuncSetAttribute((const void*)sb_phase1_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        HIP_TRY(hipFuncSetAttribute((const void*)sb_phase3_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         c->sb_ok = true;
-        if (const char* st = getenv("DDPG_SB_STAMPS"))
-          if (atoi(st)) {
-            HIP_TRY(hipMalloc(&c->sb_stamps, 16 * sizeof(unsigned long long)));
-            HIP_TRY(hipMemset(c->sb_stamps, 0, 16 * sizeof(unsigned long long)));
-          }
       }
     }
     HIP_TRY(hipDeviceSynchronize());
@@ -1134,23 +1153,6 @@ void ddpg_destroy(ddpg_ctx* c) {
 int ddpg_sync(ddpg_ctx* c) {
   return guard(c, [&] {
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->sb_stamps) {  // diagnostic: section cycle counts of the last small-batch step
-      unsigned long long t[16];
-      HIP_TRY(hipMemcpy(t, c->sb_stamps, sizeof t, hipMemcpyDeviceToHost));
-      fprintf(stderr, "[sb stamps] phase1:");
-      unsigned long long prev = t[15];
-      for (int i = 0; i <= 5; ++i) {
-        fprintf(stderr, " %llu", t[i] - prev);
-        prev = t[i];
-      }
-      fprintf(stderr, " | phase3:");
-      prev = t[14];
-      for (int i = 8; i <= 13; ++i) {
-        fprintf(stderr, " %llu", t[i] - prev);
-        prev = t[i];
-      }
-      fprintf(stderr, "\n");
-    }
   });
 }
 
@@ -1210,6 +1212,7 @@ int ddpg_set_params(ddpg_ctx* c, int which, const float* host, size_t n) {
     for (int i = 0; i < nt; ++i) tot += ts[i].count();
     if (n != tot) throw einval("param set %d expects %zu floats, got %zu", which, tot, n);
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->sb_shadow_ok = false;
     size_t o = 0;
     for (int i = 0; i < nt; ++i) {
       HIP_TRY(hipMemcpy(base + ts[i].off, host + o, ts[i].count() * 4, hipMemcpyHostToDevice));
@@ -1603,8 +1606,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
       try {
         HIP_TRY(hipMemcpyAsync(c->d_slots, g.h_idx, (size_t)B * sizeof(int),
                                hipMemcpyHostToDevice, c->stream));
-        gather_launch(c, rb, B);
-        learner_step_any(c, B, inv_b);
+        learner_step_any(c, rb, B, inv_b);
       } catch (...) {
         (void)hipStreamEndCapture(c->stream, &graph);
         throw;
@@ -1627,8 +1629,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     HIP_TRY(hipMemcpyAsync(c->d_slots, hs, (size_t)B * sizeof(int), hipMemcpyHostToDevice,
                            c->stream));
     HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
-    gather_launch(c, rb, B);
-    learner_step_any(c, B, inv_b);
+    learner_step_any(c, rb, B, inv_b);
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
   if (stats) {
