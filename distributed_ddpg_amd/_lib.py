@@ -12,7 +12,8 @@ import numpy as np
 import torch  # noqa: F401  (must precede the library load; see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libddpg_hip.so")
+# DDPG_LIB_PATH: load an alternative build (tuning experiments only)
+LIB_PATH = os.environ.get("DDPG_LIB_PATH") or os.path.join(_HERE, "libddpg_hip.so")
 
 DDPG_OK = 0
 DDPG_EINVAL, DDPG_EHIP, DDPG_ENOMEM, DDPG_ESTATE, DDPG_ECOMM = -1, -2, -3, -4, -5

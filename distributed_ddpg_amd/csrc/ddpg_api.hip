@@ -187,12 +187,16 @@ struct ddpg_ctx {
   // small-batch fused path (small_batch.h): eligible dims, per-WG gradient slabs
   bool sb_ok = false;
   int sb_max_b = 0;
-  float* sb_part = nullptr;   // [ceil(sb_max_b / SB_R)][L.total]
+  float* sb_save = nullptr;   // per-row tensors the weight gradients read (SbSave)
+  SbSave sb_sv{};
+  SbGradTab sb_tab[2]{};      // weight-gradient tables: actor, critic
   float* sb_misc = nullptr;   // alpha[2] | stat_part[2 * G]
   float* sb_whT = nullptr;    // [CH2][2 CH1] critic Wh^T shadow
   float* sb_w2T = nullptr;    // [AH2][AH1]   actor W2^T shadow
   bool sb_shadow_ok = false;  // cleared by every theta write outside the small path
   size_t sb_smem = 0;         // dynamic LDS bytes of the phase kernels
+  int sb_xstride = 1;         // XCD packing of the phase kernels (env DDPG_SB_XCD=1: on)
+  unsigned long long* sb_stamps = nullptr;  // diagnostic (env DDPG_SB_STAMPS=1)
 
   // comm
   ncclComm_t comm = nullptr;
@@ -783,18 +787,24 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC, 3);
 }
 
+// Rebuild the W^T shadows of the small path after a parameter write outside
+// it.  Eager (never captured into a step graph): the graph itself keeps the
+// shadows current through sb_wgrad_adam.
+static void sb_refresh_shadows(ddpg_ctx* c) {
+  if (!c->sb_ok || c->sb_shadow_ok) return;
+  const Layout& L = c->L;
+  hipLaunchKernelGGL(sb_transpose_kernel, dim3(64), dim3(256), 0, c->stream,
+                     c->theta + L.c[CWH].off, 2 * c->CH1, c->CH2, c->sb_whT);
+  hipLaunchKernelGGL(sb_transpose_kernel, dim3(64), dim3(256), 0, c->stream,
+                     c->theta + L.a[AW2].off, c->AH1, c->AH2, c->sb_w2T);
+  HIP_TRY(hipGetLastError());
+  c->sb_shadow_ok = true;
+}
+
 // Small-batch learner step: 4 launches (small_batch.h); the gather from the
 // replay ring is fused into the phase kernels (slots already in c->d_slots).
 static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   const Layout& L = c->L;
-  if (!c->sb_shadow_ok) {  // a parameter write outside this path: rebuild the W^T shadows
-    hipLaunchKernelGGL(sb_transpose_kernel, dim3(64), dim3(256), 0, c->cur,
-                       c->theta + L.c[CWH].off, 2 * c->CH1, c->CH2, c->sb_whT);
-    hipLaunchKernelGGL(sb_transpose_kernel, dim3(64), dim3(256), 0, c->cur,
-                       c->theta + L.a[AW2].off, c->AH1, c->AH2, c->sb_w2T);
-    HIP_TRY(hipGetLastError());
-    c->sb_shadow_ok = true;
-  }
   SbArgs a;
   memset(&a, 0, sizeof a);
   a.B = B;
@@ -805,10 +815,7 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   a.CH1 = c->CH1;
   a.CH2 = c->CH2;
   a.LX = rup(std::max(c->S, c->A), 4);
-  a.LA = rup(std::max(c->AH1, 2 * c->CH1), 4);
-  a.LB = rup(std::max(c->AH2, c->CH2), 4);
-  a.LC = rup(2 * c->CH1, 4);
-  a.LD = rup(std::max(c->CH2, c->AH2), 4);
+  a.LW = rup(std::max(std::max(c->AH1, c->AH2), std::max(2 * c->CH1, c->CH2)), 4);
   a.inv_b = inv_b;
   a.gamma = c->cfg.gamma;
   a.scale = c->cfg.action_scale;
@@ -833,8 +840,7 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   a.adam_v = c->adam_v;
   a.whT = c->sb_whT;
   a.w2T = c->sb_w2T;
-  a.part = c->sb_part;
-  a.PT = (long long)L.total;
+  a.sv = c->sb_sv;
   a.pw = c->dpw;
   a.alpha = c->sb_misc;
   a.stat_part = c->sb_misc + 4;
@@ -853,34 +859,34 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   a.cbh = L.c[CBH].off;
   a.cWo = L.c[CWO].off;
   a.cbo = L.c[CBO].off;
-  a.actor_begin = L.actor_begin;
-  a.actor_end = L.actor_end;
-  a.critic_begin = L.critic_begin;
-  a.critic_end = L.critic_end;
+  a.stamps = c->sb_stamps;
+  a.xstride = c->sb_xstride;
   const int G = ceil_div(B, SB_R);
   const long long nc = (long long)(L.critic_end - L.critic_begin);
   const long long na = (long long)(L.actor_end - L.actor_begin);
-  const int bc = (int)std::min<long long>(1024, (nc + 255) / 256);
-  const int ba = (int)std::min<long long>(1024, (na + 255) / 256);
   const double row_bytes = (2.0 * c->S + c->A + 2) * 4.0;
   {
     ProfScope ps(c, "sb_phase1", 0, 4.0 * (double)G * (L.total + nc) + B * row_bytes);
-    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G), dim3(SB_NT), c->sb_smem, c->cur, a);
+    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G * a.xstride), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
   {
-    ProfScope ps(c, "sb_reduce_adam", 0, (double)nc * 4.0 * (G + 7));
-    hipLaunchKernelGGL(sb_reduce_adam_kernel, dim3(bc), dim3(256), 0, c->cur, a, 1, G);
+    ProfScope ps(c, "sb_wgrad_adam", 2.0 * B * nc, 32.0 * nc);
+    const SbGradTab& t = c->sb_tab[1];
+    hipLaunchKernelGGL(sb_wgrad_adam_kernel, dim3(t.t[t.n].tile0), dim3(SB_GT), 0, c->cur, a, t,
+                       1, G);
     HIP_TRY(hipGetLastError());
   }
   {
     ProfScope ps(c, "sb_phase3", 0, 4.0 * (double)G * (L.total + na) + B * c->S * 4.0);
-    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G), dim3(SB_NT), c->sb_smem, c->cur, a);
+    hipLaunchKernelGGL(sb_phase3_kernel, dim3(G * a.xstride), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
   {
-    ProfScope ps(c, "sb_reduce_adam", 0, (double)na * 4.0 * (G + 7));
-    hipLaunchKernelGGL(sb_reduce_adam_kernel, dim3(ba), dim3(256), 0, c->cur, a, 0, G);
+    ProfScope ps(c, "sb_wgrad_adam", 2.0 * B * na, 32.0 * na);
+    const SbGradTab& t = c->sb_tab[0];
+    hipLaunchKernelGGL(sb_wgrad_adam_kernel, dim3(t.t[t.n].tile0), dim3(SB_GT), 0, c->cur, a, t,
+                       0, G);
     HIP_TRY(hipGetLastError());
   }
 }
@@ -954,7 +960,8 @@ static void ctx_free(ddpg_ctx* c) {
     if (g.h_idx) (void)hipHostFree(g.h_idx);
     if (g.done) (void)hipEventDestroy(g.done);
   }
-  for (void* p : {(void*)c->sb_part, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T})
+  for (void* p : {(void*)c->sb_save, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T,
+                  (void*)c->sb_stamps})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc})
@@ -1107,10 +1114,9 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     if (const char* pv = getenv("DDPG_PAR")) c->par = atoi(pv) != 0;
     {
       const int hmax = std::max(std::max(c->AH1, c->AH2), std::max(c->CH1, c->CH2));
-      const int LX = rup(std::max(c->S, c->A), 4), LA = rup(std::max(c->AH1, 2 * c->CH1), 4);
-      const int LB = rup(std::max(c->AH2, c->CH2), 4), LC = rup(2 * c->CH1, 4);
-      const int LD = rup(std::max(c->CH2, c->AH2), 4);
-      const size_t smem = sb_smem_floats(LX, LA, LB, LC, LD) * sizeof(float);
+      const int LX = rup(std::max(c->S, c->A), 4);
+      const int LW = rup(std::max(std::max(c->AH1, c->AH2), std::max(2 * c->CH1, c->CH2)), 4);
+      const size_t smem = sb_smem_floats(LX, LW) * sizeof(float);
       // vector weight streams need 4-aligned widths; 160 KiB of LDS per workgroup
       bool ok = c->world == 1 && hmax <= SB_MAXH && c->AH1 % 4 == 0 && c->AH2 % 4 == 0 &&
                 c->CH1 % 4 == 0 && c->CH2 % 4 == 0 && smem <= 160 * 1024;
@@ -1118,18 +1124,99 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       if (ok) {
         c->sb_max_b = std::min(c->Bmax, 512);
         c->sb_smem = smem;
+        if (const char* xv = getenv("DDPG_SB_XCD")) c->sb_xstride = atoi(xv) ? 8 : 1;
         const int G = ceil_div(c->sb_max_b, SB_R);
-        HIP_TRY(hipMalloc(&c->sb_part, (size_t)G * c->L.total * sizeof(float)));
-        HIP_TRY(hipMemset(c->sb_part, 0, (size_t)G * c->L.total * sizeof(float)));
+        const size_t Bp = (size_t)rup(c->sb_max_b, 4);
+        // saved tensors, feature-major [width][Bp]: xs xa cat dcat h dhp dq h1 h2 dz1 dz2 dz3
+        const size_t widths[12] = {(size_t)c->S, (size_t)c->A, 2 * (size_t)c->CH1,
+                                   2 * (size_t)c->CH1, (size_t)c->CH2, (size_t)c->CH2, 1,
+                                   (size_t)c->AH1, (size_t)c->AH2, (size_t)c->AH1,
+                                   (size_t)c->AH2, (size_t)c->A};
+        size_t tot = 0;
+        for (size_t w : widths) tot += (Bp * w + 63) / 64 * 64;
+        HIP_TRY(hipMalloc(&c->sb_save, tot * sizeof(float)));
+        HIP_TRY(hipMemset(c->sb_save, 0, tot * sizeof(float)));
+        float* ptrs[12];
+        size_t off = 0;
+        for (int k = 0; k < 12; ++k) {
+          ptrs[k] = c->sb_save + off;
+          off += (Bp * widths[k] + 63) / 64 * 64;
+        }
+        SbSave& sv = c->sb_sv;
+        sv.Bp = (int)Bp;
+        sv.xs = ptrs[0];
+        sv.xa = ptrs[1];
+        sv.cat = ptrs[2];
+        sv.dcat = ptrs[3];
+        sv.h = ptrs[4];
+        sv.dhp = ptrs[5];
+        sv.dq = ptrs[6];
+        sv.h1 = ptrs[7];
+        sv.h2 = ptrs[8];
+        sv.dz1 = ptrs[9];
+        sv.dz2 = ptrs[10];
+        sv.dz3 = ptrs[11];
+        const Layout& L = c->L;
+        const int bp = (int)Bp;
+        auto add = [bp](SbGradTab& t, const Tensor& ts, const float* X, const float* dY) {
+          SbGradT& e = t.t[t.n];
+          e.off = (long long)ts.off;
+          e.K = ts.cols == 1 && X == nullptr ? 1 : ts.rows;
+          e.N = ts.cols == 1 && X == nullptr ? ts.rows : ts.cols;
+          e.X = X;
+          e.ldx = bp;
+          e.dY = dY;
+          e.ldy = bp;
+          int tn = 1;
+          while (tn < e.N && tn < 64) tn *= 2;
+          e.TN = tn;
+          e.TK = SB_GT / tn;
+          e.tile0 = t.n ? t.t[t.n - 1].tile0 + ceil_div(t.t[t.n - 1].K, t.t[t.n - 1].TK) *
+                                                   ceil_div(t.t[t.n - 1].N, t.t[t.n - 1].TN)
+                        : 0;
+          ++t.n;
+        };
+        auto close = [](SbGradTab& t) {  // sentinel: t.t[t.n].tile0 = total tiles
+          const SbGradT& l = t.t[t.n - 1];
+          t.t[t.n].tile0 = l.tile0 + ceil_div(l.K, l.TK) * ceil_div(l.N, l.TN);
+        };
+        SbGradTab& ta = c->sb_tab[0];  // actor (networks.py:39-47)
+        ta.n = 0;
+        add(ta, L.a[AW1], sv.xs, sv.dz1);
+        add(ta, L.a[AB1], nullptr, sv.dz1);
+        add(ta, L.a[AW2], sv.h1, sv.dz2);
+        add(ta, L.a[AB2], nullptr, sv.dz2);
+        add(ta, L.a[AW3], sv.h2, sv.dz3);
+        close(ta);
+        ta.shadow = 2;
+        SbGradTab& tc = c->sb_tab[1];  // critic (networks.py:130-137)
+        tc.n = 0;
+        add(tc, L.c[CWS], sv.xs, sv.dcat);
+        add(tc, L.c[CBS], nullptr, sv.dcat);
+        add(tc, L.c[CWA], sv.xa, sv.dcat + (size_t)c->CH1 * Bp);
+        add(tc, L.c[CBA], nullptr, sv.dcat + (size_t)c->CH1 * Bp);
+        add(tc, L.c[CWH], sv.cat, sv.dhp);
+        add(tc, L.c[CBH], nullptr, sv.dhp);
+        add(tc, L.c[CWO], sv.h, sv.dq);
+        add(tc, L.c[CBO], nullptr, sv.dq);
+        close(tc);
+        tc.shadow = 4;
         HIP_TRY(hipMalloc(&c->sb_misc, (4 + 2 * (size_t)G) * sizeof(float)));
         HIP_TRY(hipMemset(c->sb_misc, 0, (4 + 2 * (size_t)G) * sizeof(float)));
         HIP_TRY(hipMalloc(&c->sb_whT, (size_t)2 * c->CH1 * c->CH2 * sizeof(float)));
         HIP_TRY(hipMalloc(&c->sb_w2T, (size_t)c->AH1 * c->AH2 * sizeof(float)));
+        ta.sh = c->sb_w2T;
+        tc.sh = c->sb_whT;
         HIP_TRY(hipFuncSetAttribute((const void*)sb_phase1_kernel,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         HIP_TRY(hipFuncSetAttribute((const void*)sb_phase3_kernel,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         c->sb_ok = true;
+        if (const char* st = getenv("DDPG_SB_STAMPS"))
+          if (atoi(st)) {
+            HIP_TRY(hipMalloc(&c->sb_stamps, 64 * sizeof(unsigned long long)));
+            HIP_TRY(hipMemset(c->sb_stamps, 0, 64 * sizeof(unsigned long long)));
+          }
       }
     }
     HIP_TRY(hipDeviceSynchronize());
@@ -1153,6 +1240,19 @@ void ddpg_destroy(ddpg_ctx* c) {
 int ddpg_sync(ddpg_ctx* c) {
   return guard(c, [&] {
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->sb_stamps) {  // diagnostic: per-op cycle counts of the last small-batch step
+      unsigned long long t[64];
+      HIP_TRY(hipMemcpy(t, c->sb_stamps, sizeof t, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[sb stamps] phase1:");
+      for (int i = 1; i <= 10; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
+      fprintf(stderr, " total %llu | phase3:", t[10] - t[0]);
+      for (int i = 33; i <= 42; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
+      fprintf(stderr, " total %llu | wgrad c:", t[42] - t[32]);
+      for (int i = 49; i <= 50; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
+      fprintf(stderr, " | wgrad a:");
+      for (int i = 57; i <= 58; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
+      fprintf(stderr, "\n");
+    }
   });
 }
 
@@ -1592,6 +1692,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   check_b(c, B);
   const int64_t* mine = idx + (size_t)c->rank * B;  // this rank's slice of the global draw
   const float inv_b = 1.0f / (float)Bg;
+  sb_refresh_shadows(c);
   // graphs: single-rank, not profiling (RCCL capture and per-kernel events stay eager)
   if (c->use_graph && c->world == 1 && !c->prof) {
     auto& g = c->gslot[c->gcur];

@@ -3,46 +3,59 @@
 //
 // At these sizes every GEMM of the large-batch path is a few-microsecond,
 // few-block launch; the step would be a chain of ~35 of them.  Here it is
-// four launches, row-parallel (one workgroup per SB_R batch rows, so the
-// forward and backward passes need no inter-workgroup exchange):
+// four launches:
 //
-//   sb_phase1  gather this WG's rows from the replay ring (+ scaler) ->
-//              target actor fwd -> target critic fwd -> TD target -> online
-//              critic fwd -> MSE loss / dQ -> critic head + dX backward ->
-//              this WG's partial critic gradients (one slab per WG, flat
-//              parameter layout).  WG 0 also computes the critic Adam step
-//              size from the beta powers and advances them (TF
-//              AdamOptimizer._finish).
-//   sb_reduce_adam(critic): g = ordered sum of the slabs -> TF ApplyAdam ->
-//              soft update of the critic target; refreshes the transposed
-//              shadow of Wh used by the dX layers.
-//   sb_phase3  online actor fwd -> updated-critic fwd at (s, mu) -> dQ/da ->
-//              actor backward -> partial actor gradients; WG 0 computes the
-//              actor step size and advances its powers.
-//   sb_reduce_adam(actor) (+ shadow of W2).
+//   sb_phase1  (row-parallel, one workgroup per SB_R batch rows): gather the
+//              rows from the replay ring (+ scaler) -> target actor fwd ->
+//              target critic fwd -> TD target -> online critic fwd -> MSE
+//              loss / dQ -> critic head + dX backward; saves the activations
+//              and output gradients the critic weight gradients need.  WG 0
+//              computes the critic Adam step size from the beta powers and
+//              advances them (TF AdamOptimizer._finish).
+//   sb_wgrad_adam(critic): every critic weight gradient dW = X^T . dY over
+//              the whole batch (one ordered fp32 sum over b per element),
+//              TF ApplyAdam, soft update of the critic target, and the
+//              transposed shadow of Wh used by the dX layers.
+//   sb_phase3  (row-parallel): online actor fwd -> updated-critic fwd at
+//              (s, mu) -> dQ/da -> actor backward; saves what the actor
+//              weight gradients need.  WG 0 computes the actor step size.
+//   sb_wgrad_adam(actor) (+ shadow of W2).
 //
-// Each dense layer is a skinny [SB_R x K] . [K x N] product: the weights are
-// read once per WG straight into VGPRs (the GEMV rule: no LDS round trip),
-// every thread owning one 4-column group of one k-slice, all of a slice's
-// loads issued before the first FMA, then an ordered LDS reduction over the
-// k-slices with the bias / activation / EluGrad epilogue.  Layers whose
-// weights would be read transposed (dX = dY . W^T) read a row-major shadow
-// W^T instead, so every weight stream is 16-B-per-lane coalesced.  Rows
-// beyond B are computed on zero inputs and masked out of every gradient and
-// stat.  The arithmetic is the same TF-semantics fp32 as the large-batch
-// path (elu / EluGrad from outputs, TanhGrad, MSE grad, ApplyAdam, soft
-// update); only the summation order differs.
+// Inside a phase, independent layers run side by side on disjoint thread
+// groups (e.g. the target actor's first layer, both critics' state branches
+// and the online critic's action branch are one level), so the dependent
+// chain is 8 levels per phase.  Each dense layer is a skinny [SB_R x K] .
+// [K x N] product: the weights are read once per WG straight into VGPRs (the
+// GEMV rule: no LDS round trip), each thread owning one 4-column group of one
+// k-slice, all of a batch's loads issued before the first FMA, then an
+// ordered LDS reduction over the k-slices with the bias / activation /
+// EluGrad epilogue.  Layers whose weights would be read transposed (dX = dY .
+// W^T) read a row-major shadow W^T instead, so every weight stream is
+// 16-B-per-lane coalesced.  Rows beyond B are computed on zero inputs and
+// never saved.  The arithmetic is the same TF-semantics fp32 as the
+// large-batch path (elu / EluGrad from outputs, TanhGrad, MSE grad,
+// ApplyAdam, soft update); only the summation order differs.
 #pragma once
 #include "common.h"
 
 namespace ddpg {
 
 constexpr int SB_R = 4;        // batch rows per workgroup
-constexpr int SB_NT = 1024;    // threads per workgroup (16 waves)
-constexpr int SB_U = 8;        // weight quads in flight per thread per batch
+#ifndef SB_NT_DEF
+#define SB_NT_DEF 512
+#endif
+constexpr int SB_NT = SB_NT_DEF;  // threads per workgroup
+#ifndef SB_U_DEF
+#define SB_U_DEF 8
+#endif
+#ifndef SB_DBUF
+#define SB_DBUF 0  // 1: two register batches (next issued before current consumed)
+#endif
+constexpr int SB_U = SB_U_DEF;  // weight quads in flight per thread per batch
 constexpr int SB_NMAX = 8;     // widest layer handled by the k-parallel thin kernel
 constexpr int SB_RED = 4 * SB_R * SB_NT;  // LDS floats of k-slice partials
 constexpr int SB_MAXH = 512;   // widest hidden layer of the small path
+constexpr int SB_GT = 256;     // threads of the weight-gradient / Adam kernel
 
 #define SB_FN __device__ __forceinline__
 
@@ -51,11 +64,24 @@ constexpr int SB_MAXH = 512;   // widest hidden layer of the small path
 typedef __attribute__((address_space(1))) f32x4 glb_v4;
 typedef __attribute__((address_space(3))) f32x4 lds_v4;
 
+// Saved per-row tensors that the weight gradients read, feature-major
+// ([feature][Bp], Bp = Bmax rounded up to 4): a workgroup stores its 4 rows of
+// a feature as one float4 and the gradient kernel reads a feature's batch
+// column as contiguous float4s.
+struct SbSave {
+  int Bp;
+  float *xs, *xa;          // [S], [A]      inputs (scaled)
+  float *cat, *dcat;       // [2 CH1]       critic concat, its gradient
+  float *h, *dhp, *dq;     // [CH2],[CH2],[1] critic hidden, its pre-act grad, dQ
+  float *h1, *h2;          // [AH1], [AH2]  actor hidden
+  float *dz1, *dz2, *dz3;  // [AH1], [AH2], [A]
+};
+
 // Per-step arguments (device pointers; offsets into the flat layout).
 struct SbArgs {
   int B;                 // local rows
   int S, A, AH1, AH2, CH1, CH2;
-  int LX, LA, LB, LC, LD;  // LDS row strides (floats, multiples of 4)
+  int LX, LW;            // LDS row strides: inputs, hidden buffers (multiples of 4)
   float inv_b, gamma, scale, tau, omt, b1, b2, lr_a, lr_c, eps;
   // replay ring + this step's slots (fused gather)
   const int* slots;
@@ -67,8 +93,7 @@ struct SbArgs {
   float* adam_v;
   float* whT;            // [CH2][2 CH1]  = critic Wh^T
   float* w2T;            // [AH2][AH1]    = actor W2^T
-  float* part;           // [G][PT] partial gradient slabs (flat param layout)
-  long long PT;          // floats per slab (= layout total)
+  SbSave sv;
   float* pw;             // beta powers [actor b1p, b2p, critic b1p, b2p]
   float* alpha;          // [actor, critic] Adam step sizes for this step
   float* stat_part;      // [G][2] loss partial, q max
@@ -76,162 +101,264 @@ struct SbArgs {
   double* acc;           // [qmax_sum, loss_sum, steps]
   long long aW1, ab1, aW2, ab2, aW3;
   long long cWs, cbs, cWa, cba, cWh, cbh, cWo, cbo;
-  long long actor_begin, actor_end, critic_begin, critic_end;
+  unsigned long long* stamps;  // diagnostic (env DDPG_SB_STAMPS): WG 0 s_memtime per level
+  // XCD packing: the grid has xstride x G blocks and only every xstride-th
+  // works, so with the hardware's round-robin block->XCD dealing all working
+  // WGs share one XCD's L2 and the weights stream from it once rather than
+  // once per XCD (speed only: any placement computes the same result)
+  int xstride;
 };
 
-// LDS floats a workgroup needs (host side: launch size and eligibility).
-inline size_t sb_smem_floats(int LX, int LA, int LB, int LC, int LD) {
-  return (size_t)SB_R * (4 * LX + LA + LB + LC + LD + 8) + SB_RED;
+// Diagnostic stamp: nothing reads it on device and no output depends on it.
+#define SB_STAMP(i)                                                              \
+  do {                                                                           \
+    if (g.stamps && blockIdx.x == 0 && threadIdx.x == 0)                         \
+      g.stamps[i] = __builtin_amdgcn_s_memtime();                                \
+  } while (0)
+
+// LDS floats a phase workgroup needs (host side: launch size and eligibility).
+inline size_t sb_smem_floats(int LX, int LW) {
+  return (size_t)SB_R * (4 * LX + 5 * LW + 8) + SB_RED + 2 * 2048;  // + biases / pw
 }
 
-// Epilogue kinds of sb_dense.
+// Activation layout in LDS: k-major, the SB_R (= 4) rows of one feature
+// contiguous (X[k*4 + r]), so one ds_read_b128 feeds a weight quad's 16 FMAs
+// and no index needs a division.  All buffer pointers below are already
+// offset to their first feature.
+static_assert(SB_R == 4, "k-major activation layout assumes 4 rows per workgroup");
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Epilogue kinds of a dense layer.
 enum { SB_NONE = 0, SB_ELU = 1, SB_POST2 = 2, SB_AUX = 3 };
 
-// Y[r][n] = epi(sum_k X[r][k] W[k*ldw + n]) for r < SB_R, n < N.
-// N, ldw multiples of 4, W 16-B aligned, N <= 4 * SB_NT.  X, Y, aux in LDS.
-//   SB_NONE  v
-//   SB_ELU   elu(v + b[n])
-//   SB_POST2 pw[n] * elu'(elu(v + b[n]))     (critic head, grad_ys = 1)
-//   SB_AUX   v * elu'(aux[r][n])             (dX . EluGrad)
-// Thread t owns column quad q = t % NQ of k-slice s = t / NQ and the k rows
-// s, s + S, s + 2S, ...; the SB_U loads of a batch are all issued before any
-// is consumed.  The k-slice partials are summed in slice order (fixed,
-// deterministic).  Y may alias aux (same element read then written by one
-// thread) but not X.  Ends with a barrier.
-SB_FN void sb_dense(const lds_f* X, int ldx, int K, const glb_f* __restrict__ W, int ldw, int N,
-                    const glb_f* __restrict__ b, int epi, const glb_f* __restrict__ pw,
-                    const lds_f* aux, int ldaux, lds_f* Y, int ldy, lds_f* red) {
-  const int tid = threadIdx.x;
-  const int NQ = N >> 2;
-  const int S = SB_NT / NQ;
-  const int q = tid % NQ, s = tid / NQ;
-  if (s < S) {
-    f32x4 acc[SB_R];
+// One skinny layer: Y[n][r] = epi(sum_k X[k][r] W(k, n)) for r < 4, n < N.
+//   dense: W(k, n) = W[k*ldw + n]; N, ldw multiples of 4, W 16-B aligned.
+//   thin (N <= SB_NMAX): W(k, n) = trans ? W[n*ldw + k] : W[k*ldw + n].
+// epi: SB_NONE v | SB_ELU elu(v + b[n]) | SB_POST2 pw[n] * elu'(elu(v + b[n]))
+//      (critic head, grad_ys = 1) | SB_AUX v * elu'(aux[n][r]) (dX . EluGrad).
+// thin: v (+ b[n]) then tanh when act_tanh.
+struct SbOp {
+  const lds_f* X;
+  int K;
+  const glb_f* W;
+  int ldw, N;
+  const glb_f* b;
+  int epi;
+  const glb_f* pw;
+  const lds_f* aux;
+  lds_f* Y;
+  bool trans, act_tanh;
+};
+
+DDPG_DEV SbOp sb_op(const lds_f* X, int K, const glb_f* W, int ldw, int N, const glb_f* b,
+                    int epi, lds_f* Y, const lds_f* aux = nullptr, const glb_f* pw = nullptr) {
+  SbOp o;
+  o.X = X;
+  o.K = K;
+  o.W = W;
+  o.ldw = ldw;
+  o.N = N;
+  o.b = b;
+  o.epi = epi;
+  o.pw = pw;
+  o.aux = aux;
+  o.Y = Y;
+  o.trans = false;
+  o.act_tanh = false;
+  return o;
+}
+
+// acc[c][r] += x[r] * w[c], as packed f32 FMAs (two rows per instruction).
+SB_FN void sb_fma4(f32x4 (&acc)[4], f32x4 x, f32x4 w) {
+  const f32x2 xl = {x[0], x[1]}, xh = {x[2], x[3]};
 #pragma unroll
-    for (int r = 0; r < SB_R; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const glb_v4* Wq = reinterpret_cast<const glb_v4*>(W) + q;
-    const int ldq = ldw >> 2;
-    for (int k0 = s; k0 < K; k0 += SB_U * S) {
-      f32x4 w[SB_U];
+  for (int c = 0; c < 4; ++c) {
+    const f32x2 wc = {w[c], w[c]};
+    f32x2 lo = {acc[c][0], acc[c][1]}, hi = {acc[c][2], acc[c][3]};
+    lo = __builtin_elementwise_fma(xl, wc, lo);
+    hi = __builtin_elementwise_fma(xh, wc, hi);
+    acc[c] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+  }
+}
+
+// Dense layer, part 1 on threads t < nt of a wave-aligned group: thread t owns
+// column quad q = t % NQ of k-slice s = t / NQ (S = min(nt / NQ, K) slices)
+// and the k rows s, s + S, ...; the SB_U loads of a batch are all issued
+// before any is consumed.  Partials go to red[s][n][r] (f32x4 per n).
+SB_FN void sb_dense_part(const SbOp& o, int t, int nt, lds_f* red) {
+  const int NQ = o.N >> 2;
+  const int S = min(nt / NQ, o.K);
+  const int q = t % NQ, s = t / NQ;
+  if (s >= S) return;
+  f32x4 acc[4];
 #pragma unroll
-      for (int u = 0; u < SB_U; ++u) w[u] = Wq[(size_t)min(k0 + u * S, K - 1) * ldq];
+  for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int K = o.K;
+  const lds_v4* X4 = reinterpret_cast<const lds_v4*>(o.X);
+  const glb_v4* Wq = reinterpret_cast<const glb_v4*>(o.W) + q;
+  const size_t step = (size_t)S * (o.ldw >> 2);  // float4s between this thread's k rows
+  const glb_v4* wp = Wq + (size_t)s * (o.ldw >> 2);
+  const int nk = (K - s + S - 1) / S;  // this thread's k rows
+  int i = 0;
+  for (; i + SB_U <= nk; i += SB_U) {
+    f32x4 w[SB_U];
 #pragma unroll
-      for (int u = 0; u < SB_U; ++u) {
-        const int k = k0 + u * S;
-        const int kk = min(k, K - 1);
+    for (int u = 0; u < SB_U; ++u) w[u] = wp[u * step];
 #pragma unroll
-        for (int r = 0; r < SB_R; ++r) {
-          const float x = k < K ? X[r * ldx + kk] : 0.f;
+    for (int u = 0; u < SB_U; ++u) sb_fma4(acc, X4[s + (i + u) * S], w[u]);
+    wp += SB_U * step;
+  }
+  if (i < nk) {  // remainder: clamped loads, masked FMAs
+    f32x4 w[SB_U];
+    const int rem = nk - i;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(x, w[u][c], acc[r][c]);
+    for (int u = 0; u < SB_U; ++u) w[u] = wp[min(u, rem - 1) * step];
+#pragma unroll
+    for (int u = 0; u < SB_U; ++u)
+      if (u < rem) sb_fma4(acc, X4[s + (i + u) * S], w[u]);
+  }
+  lds_v4* r4 = reinterpret_cast<lds_v4*>(red) + (size_t)s * o.N + 4 * q;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) r4[c] = acc[c];
+}
+
+// Dense layer, part 2: output idx = n*4 + r sums its S partials in slice
+// order (loads batched 8 at a time, adds sequential) and applies the epilogue.
+SB_FN void sb_dense_epi(const SbOp& o, int t, int nt, const lds_f* red, const lds_f* bl,
+                        const lds_f* pwl) {
+  const int N = o.N;
+  const int S = min(nt / (N >> 2), o.K);
+  const int stride = 4 * N;
+  for (int idx = t; idx < 4 * N; idx += nt) {
+    const int n = idx >> 2;
+    const lds_f* pr = red + idx;
+    float v = 0.f;
+    int j = 0;
+    for (; j + 8 <= S; j += 8) {
+      float p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p[u] = pr[(j + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += p[u];
+    }
+    for (; j < S; ++j) v += pr[j * stride];
+    if (o.epi == SB_ELU) {
+      v = elu_f(__fadd_rn(v, bl[n]));
+    } else if (o.epi == SB_POST2) {
+      v = __fmul_rn(pwl[n], elu_grad_factor(elu_f(__fadd_rn(v, bl[n]))));
+    } else if (o.epi == SB_AUX) {
+      v = __fmul_rn(v, elu_grad_factor(o.aux[idx]));
+    }
+    o.Y[idx] = v;
+  }
+}
+
+// Thin layer, part 1: k-parallel over the group, wave reduction, one partial
+// per (group wave, output, row) in red.
+SB_FN void sb_thin_part(const SbOp& o, int t, int nt, lds_f* red) {
+  float acc[SB_NMAX][4];
+#pragma unroll
+  for (int n = 0; n < SB_NMAX; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[n][r] = 0.f;
+  const lds_v4* X4 = reinterpret_cast<const lds_v4*>(o.X);
+  for (int k = t; k < o.K; k += nt) {
+    const f32x4 x = X4[k];
+#pragma unroll
+    for (int n = 0; n < SB_NMAX; ++n) {
+      if (n < o.N) {
+        const float w = o.trans ? o.W[(size_t)n * o.ldw + k] : o.W[(size_t)k * o.ldw + n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[n][r] = fmaf(x[r], w, acc[n][r]);
+      }
+    }
+  }
+  const int lane = t & 63, wave = t >> 6;
+#pragma unroll
+  for (int n = 0; n < SB_NMAX; ++n) {
+    if (n < o.N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[n][r];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0) red[(wave * SB_NMAX + n) * 4 + r] = v;
+      }
+    }
+  }
+}
+
+SB_FN void sb_thin_epi(const SbOp& o, int t, int nt, const lds_f* red) {
+  if (t < 4 * o.N) {
+    const int n = t >> 2;
+    float v = 0.f;
+    for (int w = 0; w < nt / 64; ++w) v += red[w * SB_NMAX * 4 + t];
+    if (o.b) v = __fadd_rn(v, o.b[n]);
+    if (o.act_tanh) v = tanhf(v);
+    o.Y[t] = v;
+  }
+}
+
+// One level of NOPS independent layers on NOPS equal wave-aligned thread
+// groups, each with its own slice of red and of the bias area (the bias and
+// pw vectors are loaded before the weights, so their round trip hides behind
+// the weights', and parked in LDS for the epilogue).  Ends with a barrier.
+constexpr int SB_BIAS = 2048;  // LDS floats for biases (+ as many for pw)
+template <int NOPS>
+SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* red) {
+  constexpr int nt = SB_NT / NOPS;
+  constexpr int rs = SB_RED / NOPS;
+  constexpr int bs = SB_BIAS / NOPS;
+  lds_f* bias = red + SB_RED;
+  const int grp = threadIdx.x / nt, t = threadIdx.x - grp * nt;
+#pragma unroll
+  for (int i = 0; i < NOPS; ++i)
+    if (grp == i) {
+      if (thin[i]) {
+        sb_thin_part(ops[i], t, nt, red + i * rs);
+      } else {
+        const SbOp& o = ops[i];
+        const bool hb = o.epi == SB_ELU || o.epi == SB_POST2;
+        float bv[4], pv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = t + j * nt;
+          bv[j] = (hb && n < o.N) ? o.b[n] : 0.f;
+          pv[j] = (o.epi == SB_POST2 && n < o.N) ? o.pw[n] : 0.f;
+        }
+        sb_dense_part(o, t, nt, red + i * rs);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = t + j * nt;
+          if (n < o.N && n < bs) {
+            bias[i * bs + n] = bv[j];
+            bias[SB_BIAS + i * bs + n] = pv[j];
+          }
         }
       }
     }
-#pragma unroll
-    for (int r = 0; r < SB_R; ++r)
-      *reinterpret_cast<lds_v4*>(red + (s * SB_R + r) * N + 4 * q) = acc[r];
-  }
   __syncthreads();
-  for (int idx = tid; idx < SB_R * N; idx += SB_NT) {
-    const int r = idx / N, n = idx - r * N;
-    float v = 0.f;
-    for (int j = 0; j < S; ++j) v += red[(j * SB_R + r) * N + n];
-    if (epi == SB_ELU) {
-      v = elu_f(__fadd_rn(v, b[n]));
-    } else if (epi == SB_POST2) {
-      v = __fmul_rn(pw[n], elu_grad_factor(elu_f(__fadd_rn(v, b[n]))));
-    } else if (epi == SB_AUX) {
-      v = __fmul_rn(v, elu_grad_factor(aux[r * ldaux + n]));
+#pragma unroll
+  for (int i = 0; i < NOPS; ++i)
+    if (grp == i) {
+      if (thin[i]) sb_thin_epi(ops[i], t, nt, red + i * rs);
+      else sb_dense_epi(ops[i], t, nt, red + i * rs, bias + i * bs, bias + SB_BIAS + i * bs);
     }
-    Y[r * ldy + n] = v;
-  }
   __syncthreads();
 }
 
-// Thin layers (N <= SB_NMAX outputs: actor W3, critic Wo, critic Wa^T):
-// k-parallel over the whole workgroup, then a block reduction.
-// trans: W is [N][K] (X . W^T).  Y[r][n] = act(sum_k X[r][k] W(k, n) + b[n]),
-// act 0 none, 2 tanh.  Ends with a barrier.
-SB_FN void sb_thin(const lds_f* X, int ldx, int K, const glb_f* __restrict__ W, int ldw,
-                   bool trans, const glb_f* __restrict__ b, int N, lds_f* Y, int ldy, int act,
-                   lds_f* red) {
-  float acc[SB_R][SB_NMAX];
-#pragma unroll
-  for (int r = 0; r < SB_R; ++r)
-#pragma unroll
-    for (int n = 0; n < SB_NMAX; ++n) acc[r][n] = 0.f;
-  for (int k = threadIdx.x; k < K; k += SB_NT) {
-    float xv[SB_R];
-#pragma unroll
-    for (int r = 0; r < SB_R; ++r) xv[r] = X[r * ldx + k];
-#pragma unroll
-    for (int n = 0; n < SB_NMAX; ++n) {
-      if (n < N) {
-        const float w = trans ? W[(size_t)n * ldw + k] : W[(size_t)k * ldw + n];
-#pragma unroll
-        for (int r = 0; r < SB_R; ++r) acc[r][n] = fmaf(xv[r], w, acc[r][n]);
-      }
-    }
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int r = 0; r < SB_R; ++r)
-#pragma unroll
-    for (int n = 0; n < SB_NMAX; ++n) {
-      if (n < N) {
-        float v = acc[r][n];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0) red[(wave * SB_R + r) * SB_NMAX + n] = v;
-      }
-    }
-  __syncthreads();
-  if (threadIdx.x < SB_R * N) {
-    const int r = threadIdx.x / N, n = threadIdx.x - r * N;
-    float v = 0.f;
-    for (int w = 0; w < SB_NT / 64; ++w) v += red[(w * SB_R + r) * SB_NMAX + n];
-    if (b) v = __fadd_rn(v, b[n]);
-    if (act == 2) v = tanhf(v);
-    Y[r * ldy + n] = v;
-  }
-  __syncthreads();
+SB_FN void sb_dense1(const SbOp& o, lds_f* red) {
+  const SbOp ops[1] = {o};
+  const bool th[1] = {false};
+  sb_level<1>(ops, th, red);
 }
 
-// out[i*N + j] = sum_r X[r][i] dY[r][j] (i < Kin, j < N) into this WG's global
-// gradient slab; db[j] = sum_r dY[r][j] when db.  Masked rows of dY are zero.
-// N % 4 == 0: one float4 store per (i, column quad); otherwise scalar.
-SB_FN void sb_wgrad(const lds_f* X, int ldx, int Kin, const lds_f* dY, int ldy, int N,
-                    glb_f* __restrict__ out, glb_f* __restrict__ db) {
-  if ((N & 3) == 0) {
-    const int NQ = N >> 2;
-    for (int p = threadIdx.x; p < Kin * NQ; p += SB_NT) {
-      const int i = p / NQ, j = 4 * (p - i * NQ);
-      f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < SB_R; ++r) {
-        const float x = X[r * ldx + i];
-        const f32x4 d = *reinterpret_cast<const lds_v4*>(dY + r * ldy + j);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) sacc[c] = fmaf(x, d[c], sacc[c]);
-      }
-      *reinterpret_cast<glb_v4*>(out + (size_t)i * N + j) = sacc;
-    }
-  } else {
-    for (int p = threadIdx.x; p < Kin * N; p += SB_NT) {
-      const int i = p / N, j = p - i * N;
-      float sacc = 0.f;
-#pragma unroll
-      for (int r = 0; r < SB_R; ++r) sacc = fmaf(X[r * ldx + i], dY[r * ldy + j], sacc);
-      out[p] = sacc;
-    }
-  }
-  if (db)
-    for (int j = threadIdx.x; j < N; j += SB_NT) {
-      float sacc = 0.f;
-#pragma unroll
-      for (int r = 0; r < SB_R; ++r) sacc += dY[r * ldy + j];
-      db[j] = sacc;
-    }
+SB_FN void sb_thin1(SbOp o, bool trans, bool act_tanh, lds_f* red) {
+  o.trans = trans;
+  o.act_tanh = act_tanh;
+  const SbOp ops[1] = {o};
+  const bool th[1] = {true};
+  sb_level<1>(ops, th, red);
 }
 
 // TF ApplyAdam step size from the beta powers, then _finish's power update.
@@ -242,228 +369,312 @@ DDPG_DEV void sb_alpha_and_advance(float* pw, float* alpha, float lr, float b1, 
   pw[1] = __fmul_rn(b2p, b2);
 }
 
-// dst[r][k] = ring[slot(r0 + r)][k] (k < cols), zero beyond cols up to ldd and
+// dst[k][r] = ring[slot(r0 + r)][k] for k < cols, zero up to ldk features and
 // for rows past `valid`; the scaler (x - mean) / scale in fp64 when mean.
-DDPG_DEV void sb_gather(lds_f* dst, int ldd, const float* __restrict__ ring, int cols,
+// save (optional): the valid rows also go to save[k * Bp + r0 + r].
+DDPG_DEV void sb_gather(lds_f* dst, int ldk, const float* __restrict__ ring, int cols,
                         const int* __restrict__ slots, int r0, int valid,
-                        const double* __restrict__ mean, const double* __restrict__ sdev) {
-  for (int idx = threadIdx.x; idx < SB_R * ldd; idx += SB_NT) {
-    const int r = idx / ldd, k = idx - r * ldd;
+                        const double* __restrict__ mean, const double* __restrict__ sdev,
+                        float* __restrict__ save, int Bp) {
+  for (int idx = threadIdx.x; idx < 4 * ldk; idx += SB_NT) {
+    const int k = idx >> 2, r = idx & 3;
     float x = 0.f;
     if (r < valid && k < cols) {
       x = ring[(size_t)slots[r0 + r] * cols + k];
       if (mean) x = (float)(((double)x - mean[k]) / sdev[k]);
+      if (save) save[(size_t)k * Bp + r0 + r] = x;
     }
     dst[idx] = x;
   }
 }
 
+// save[k][r0 .. r0 + 3] = src[k][0 .. 3] (feature-major, one float4 per
+// feature; rows past B land in the padding that no reader sums).
+DDPG_DEV void sb_save(float* __restrict__ save, int Bp, int cols, const lds_f* src, int r0) {
+  const lds_v4* s4 = reinterpret_cast<const lds_v4*>(src);
+  for (int k = threadIdx.x; k < cols; k += SB_NT)
+    *reinterpret_cast<f32x4*>(save + (size_t)k * Bp + r0) = s4[k];
+}
+
 __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * SB_R;
+  if (blockIdx.x % g.xstride) return;
+  const int wg = blockIdx.x / g.xstride;
+  const int r0 = wg * SB_R;
   const int valid = min(SB_R, g.B - r0);
+  const int LX = g.LX, LW = g.LW;
   lds_f* red = LDS(sm);
-  lds_f* xs = red + SB_RED;
-  lds_f* xs2 = xs + SB_R * g.LX;
-  lds_f* xa = xs2 + SB_R * g.LX;
-  lds_f* ta2 = xa + SB_R * g.LX;
-  lds_f* bufA = ta2 + SB_R * g.LX;
-  lds_f* bufB = bufA + SB_R * g.LA;
-  lds_f* bufC = bufB + SB_R * g.LB;
-  lds_f* bufD = bufC + SB_R * g.LC;
-  lds_f* col = bufD + SB_R * g.LD;  // [SB_R][8]: q', y, q, dq, r, t
+  lds_f* xs = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
+  lds_f* xs2 = xs + 4 * LX;
+  lds_f* xa = xs2 + 4 * LX;
+  lds_f* ta2 = xa + 4 * LX;
+  lds_f* b1 = ta2 + 4 * LX;    // [LW][4] target h1, then target hh
+  lds_f* b2 = b1 + 4 * LW;     // target h2, then dhp
+  lds_f* b3 = b2 + 4 * LW;     // target cat, then dcat
+  lds_f* cat = b3 + 4 * LW;    // online cat
+  lds_f* h = cat + 4 * LW;     // online critic hidden
+  lds_f* col = h + 4 * LW;     // [8][4]: q', y, q, dq, r, t (feature-major too)
   const glb_f* T = GLB(g.target);
   const glb_f* P = GLB(g.theta);
-  glb_f* part = GLB(g.part) + (size_t)blockIdx.x * g.PT;
+  SB_STAMP(0);
 
-  if (blockIdx.x == 0 && tid == 0) sb_alpha_and_advance(g.pw + 2, g.alpha + 1, g.lr_c, g.b1, g.b2);
-  sb_gather(xs, g.LX, g.rs, g.S, g.slots, r0, valid, g.mean, g.sdev);
-  sb_gather(xs2, g.LX, g.rs2, g.S, g.slots, r0, valid, g.mean, g.sdev);
-  sb_gather(xa, g.LX, g.ra, g.A, g.slots, r0, valid, nullptr, nullptr);
-  // ta2 is written only in its first A columns; the padding up to LX must be 0
-  for (int idx = tid; idx < SB_R * g.LX; idx += SB_NT) ta2[idx] = 0.f;
-  if (tid < SB_R) {
+  if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw + 2, g.alpha + 1, g.lr_c, g.b1, g.b2);
+  sb_gather(xs, LX, g.rs, g.S, g.slots, r0, valid, g.mean, g.sdev, g.sv.xs, g.sv.Bp);
+  sb_gather(xs2, LX, g.rs2, g.S, g.slots, r0, valid, g.mean, g.sdev, nullptr, 0);
+  sb_gather(xa, LX, g.ra, g.A, g.slots, r0, valid, nullptr, nullptr, g.sv.xa, g.sv.Bp);
+  if (tid < 4) {
     const bool ok = tid < valid;
-    col[tid * 8 + 4] = ok ? g.rr[g.slots[r0 + tid]] : 0.f;
-    col[tid * 8 + 5] = ok ? g.rt[g.slots[r0 + tid]] : 0.f;
+    col[4 * 4 + tid] = ok ? g.rr[g.slots[r0 + tid]] : 0.f;
+    col[5 * 4 + tid] = ok ? g.rt[g.slots[r0 + tid]] : 0.f;
   }
   __syncthreads();
-  // ---- target actor: ta2 = scale * tanh(elu(elu(s2 W1 + b1) W2 + b2) W3)   ddpg.py:90
-  sb_dense(xs2, g.LX, g.S, T + g.aW1, g.AH1, g.AH1, T + g.ab1, SB_ELU, nullptr, nullptr, 0, bufA,
-           g.LA, red);
-  sb_dense(bufA, g.LA, g.AH1, T + g.aW2, g.AH2, g.AH2, T + g.ab2, SB_ELU, nullptr, nullptr, 0,
-           bufB, g.LB, red);
-  sb_thin(bufB, g.LB, g.AH2, T + g.aW3, g.A, false, nullptr, g.A, ta2, g.LX, 2, red);
-  for (int idx = tid; idx < SB_R * g.A; idx += SB_NT) {
-    const int r = idx / g.A, a = idx - r * g.A;
-    ta2[r * g.LX + a] = __fmul_rn(ta2[r * g.LX + a], g.scale);
+  SB_STAMP(1);
+  {  // L1: target h1 | target state branch | online state branch | online action branch
+    const SbOp ops[4] = {sb_op(xs2, g.S, T + g.aW1, g.AH1, g.AH1, T + g.ab1, SB_ELU, b1),
+                         sb_op(xs2, g.S, T + g.cWs, g.CH1, g.CH1, T + g.cbs, SB_ELU, b3),
+                         sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat),
+                         sb_op(xa, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU,
+                               cat + 4 * g.CH1)};
+    const bool th[4] = {false, false, false, false};
+    sb_level<4>(ops, th, red);
   }
+  SB_STAMP(2);
+  {  // L2: target h2 | online critic hidden (networks.py:154-156)
+    const SbOp ops[2] = {sb_op(b1, g.AH1, T + g.aW2, g.AH2, g.AH2, T + g.ab2, SB_ELU, b2),
+                         sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_ELU, h)};
+    const bool th[2] = {false, false};
+    sb_level<2>(ops, th, red);
+  }
+  SB_STAMP(3);
+  {  // L3: target actor out o' = tanh(h2' W3') | online q = h Wo + bo
+    SbOp ops[2] = {sb_op(b2, g.AH2, T + g.aW3, g.A, g.A, nullptr, SB_NONE, ta2),
+                   sb_op(h, g.CH2, P + g.cWo, 1, 1, P + g.cbo, SB_NONE, col + 2 * 4)};
+    ops[0].act_tanh = true;
+    const bool th[2] = {true, true};
+    sb_level<2>(ops, th, red);
+  }
+  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) ta2[idx] = __fmul_rn(ta2[idx], g.scale);
   __syncthreads();
-  // ---- target critic: q' and y = t ? r : r + gamma q'
-  sb_dense(xs2, g.LX, g.S, T + g.cWs, g.CH1, g.CH1, T + g.cbs, SB_ELU, nullptr, nullptr, 0, bufC,
-           g.LC, red);
-  sb_dense(ta2, g.LX, g.A, T + g.cWa, g.CH1, g.CH1, T + g.cba, SB_ELU, nullptr, nullptr, 0,
-           bufC + g.CH1, g.LC, red);
-  sb_dense(bufC, g.LC, 2 * g.CH1, T + g.cWh, g.CH2, g.CH2, T + g.cbh, SB_ELU, nullptr, nullptr, 0,
-           bufD, g.LD, red);
-  sb_thin(bufD, g.LD, g.CH2, T + g.cWo, 1, false, T + g.cbo, 1, col + 0, 8, 0, red);
-  if (tid < SB_R) {
-    const float rr = col[tid * 8 + 4], tt = col[tid * 8 + 5];
-    col[tid * 8 + 1] = tt != 0.f ? rr : __fadd_rn(rr, __fmul_rn(g.gamma, col[tid * 8 + 0]));
-  }
-  // ---- online critic forward (networks.py:147-162)
-  sb_dense(xs, g.LX, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, nullptr, nullptr, 0, bufC,
-           g.LC, red);
-  sb_dense(xa, g.LX, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, nullptr, nullptr, 0,
-           bufC + g.CH1, g.LC, red);
-  sb_dense(bufC, g.LC, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_ELU, nullptr, nullptr, 0,
-           bufD, g.LD, red);
-  sb_thin(bufD, g.LD, g.CH2, P + g.cWo, 1, false, P + g.cbo, 1, col + 2, 8, 0, red);
-  // ---- MSE loss / dQ (networks.py:136): dq = -((1/B) * (2 * (y - q)))
+  SB_STAMP(4);
+  // L4: target action branch; L5: target critic hidden; L6: q'
+  sb_dense1(sb_op(ta2, g.A, T + g.cWa, g.CH1, g.CH1, T + g.cba, SB_ELU, b3 + 4 * g.CH1), red);
+  SB_STAMP(5);
+  sb_dense1(sb_op(b3, 2 * g.CH1, T + g.cWh, g.CH2, g.CH2, T + g.cbh, SB_ELU, b1), red);
+  SB_STAMP(6);
+  sb_thin1(sb_op(b1, g.CH2, T + g.cWo, 1, 1, T + g.cbo, SB_NONE, col), false, false, red);
+  SB_STAMP(7);
+  // ---- y = t ? r : r + gamma q' (ddpg.py:92-97), MSE loss / dQ (networks.py:136):
+  // dq = -((1/B) * (2 * (y - q)))
   if (tid == 0) {
     float lsum = 0.f, qmax = -INFINITY;
-    for (int r = 0; r < SB_R; ++r) {
-      const float q = col[r * 8 + 2];
-      const float d = __fsub_rn(col[r * 8 + 1], q);
+    for (int r = 0; r < 4; ++r) {
+      const float rr = col[4 * 4 + r], tt = col[5 * 4 + r];
+      const float y = tt != 0.f ? rr : __fadd_rn(rr, __fmul_rn(g.gamma, col[r]));
+      const float q = col[2 * 4 + r];
+      const float d = __fsub_rn(y, q);
       const bool ok = r < valid;
-      col[r * 8 + 3] = ok ? -__fmul_rn(g.inv_b, __fmul_rn(2.f, d)) : 0.f;
+      const float dq = ok ? -__fmul_rn(g.inv_b, __fmul_rn(2.f, d)) : 0.f;
+      col[3 * 4 + r] = dq;
       if (ok) {
+        g.sv.dq[r0 + r] = dq;
         lsum += __fmul_rn(d, d);
         qmax = fmaxf(qmax, q);
       }
     }
-    g.stat_part[blockIdx.x * 2 + 0] = lsum;
-    g.stat_part[blockIdx.x * 2 + 1] = qmax;
+    g.stat_part[wg * 2 + 0] = lsum;
+    g.stat_part[wg * 2 + 1] = qmax;
   }
   __syncthreads();
-  // ---- critic head backward: dhp = dq * Wo * elu'(h) -> bufB
-  for (int idx = tid; idx < SB_R * g.CH2; idx += SB_NT) {
-    const int r = idx / g.CH2, j = idx - r * g.CH2;
-    bufB[r * g.LB + j] = __fmul_rn(__fmul_rn(col[r * 8 + 3], P[g.cWo + j]),
-                                   elu_grad_factor(bufD[r * g.LD + j]));
+  // ---- critic head backward: dhp = dq * Wo * elu'(h) -> b2
+  for (int idx = tid; idx < 4 * g.CH2; idx += SB_NT) {
+    const int j = idx >> 2, r = idx & 3;
+    b2[idx] = __fmul_rn(__fmul_rn(col[3 * 4 + r], P[g.cWo + j]), elu_grad_factor(h[idx]));
   }
   __syncthreads();
-  // dcat = dhp . Wh^T * elu'(cat) -> bufA   (Wh^T read from its row-major shadow)
-  sb_dense(bufB, g.LB, g.CH2, GLB(g.whT), 2 * g.CH1, 2 * g.CH1, nullptr, SB_AUX, nullptr, bufC,
-           g.LC, bufA, g.LA, red);
-  // ---- partial critic gradients (this WG's rows)
-  sb_wgrad(xs, g.LX, g.S, bufA, g.LA, g.CH1, part + g.cWs, part + g.cbs);
-  sb_wgrad(xa, g.LX, g.A, bufA + g.CH1, g.LA, g.CH1, part + g.cWa, part + g.cba);
-  sb_wgrad(bufC, g.LC, 2 * g.CH1, bufB, g.LB, g.CH2, part + g.cWh, part + g.cbh);
-  for (int j = tid; j < g.CH2; j += SB_NT) {
-    float sacc = 0.f;
-    for (int r = 0; r < SB_R; ++r) sacc = fmaf(bufD[r * g.LD + j], col[r * 8 + 3], sacc);
-    part[g.cWo + j] = sacc;
-  }
-  if (tid == 0) {
-    float sacc = 0.f;
-    for (int r = 0; r < SB_R; ++r) sacc += col[r * 8 + 3];
-    part[g.cbo] = sacc;
+  SB_STAMP(8);
+  // L7: dcat = dhp . Wh^T * elu'(cat) -> b3   (Wh^T read from its row-major shadow)
+  sb_dense1(sb_op(b2, g.CH2, GLB(g.whT), 2 * g.CH1, 2 * g.CH1, nullptr, SB_AUX, b3, cat), red);
+  SB_STAMP(9);
+  sb_save(g.sv.cat, g.sv.Bp, 2 * g.CH1, cat, r0);
+  sb_save(g.sv.dcat, g.sv.Bp, 2 * g.CH1, b3, r0);
+  sb_save(g.sv.h, g.sv.Bp, g.CH2, h, r0);
+  sb_save(g.sv.dhp, g.sv.Bp, g.CH2, b2, r0);
+  if (g.stamps) {
+    __syncthreads();
+    SB_STAMP(10);
   }
 }
 
 __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * SB_R;
+  if (blockIdx.x % g.xstride) return;
+  const int wg = blockIdx.x / g.xstride;
+  const int r0 = wg * SB_R;
   const int valid = min(SB_R, g.B - r0);
+  const int LX = g.LX, LW = g.LW;
   lds_f* red = LDS(sm);
-  lds_f* xs = red + SB_RED;
-  lds_f* o = xs + SB_R * g.LX;
-  lds_f* mu = o + SB_R * g.LX;
-  lds_f* dz3 = mu + SB_R * g.LX;
-  lds_f* bufA = dz3 + SB_R * g.LX;
-  lds_f* bufB = bufA + SB_R * g.LA;
-  lds_f* bufC = bufB + SB_R * g.LB;
-  lds_f* bufD = bufC + SB_R * g.LC;
+  lds_f* xs = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
+  lds_f* o = xs + 4 * LX;
+  lds_f* mu = o + 4 * LX;
+  lds_f* dz3 = mu + 4 * LX;
+  lds_f* h1 = dz3 + 4 * LX;    // [LW][4]
+  lds_f* h2 = h1 + 4 * LW;
+  lds_f* cat = h2 + 4 * LW;    // critic concat at (s, mu); later dz1
+  lds_f* dh = cat + 4 * LW;    // dhp2, later dz2
   const glb_f* P = GLB(g.theta);
-  glb_f* part = GLB(g.part) + (size_t)blockIdx.x * g.PT;
+  SB_STAMP(32);
 
-  if (blockIdx.x == 0 && tid == 0) sb_alpha_and_advance(g.pw, g.alpha, g.lr_a, g.b1, g.b2);
-  sb_gather(xs, g.LX, g.rs, g.S, g.slots, r0, valid, g.mean, g.sdev);
-  // o / mu / dz3 are written only in their first A columns
-  for (int idx = tid; idx < 3 * SB_R * g.LX; idx += SB_NT) o[idx] = 0.f;
-  __syncthreads();
-  // ---- online actor forward (current actor params): h1 -> bufA, h2 -> bufB, o, mu
-  sb_dense(xs, g.LX, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, nullptr, nullptr, 0, bufA,
-           g.LA, red);
-  sb_dense(bufA, g.LA, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, nullptr, nullptr, 0,
-           bufB, g.LB, red);
-  sb_thin(bufB, g.LB, g.AH2, P + g.aW3, g.A, false, nullptr, g.A, o, g.LX, 2, red);
-  for (int idx = tid; idx < SB_R * g.A; idx += SB_NT) {
-    const int r = idx / g.A, a = idx - r * g.A;
-    mu[r * g.LX + a] = __fmul_rn(o[r * g.LX + a], g.scale);
+  if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw, g.alpha, g.lr_a, g.b1, g.b2);
+  for (int idx = tid; idx < 4 * LX; idx += SB_NT) {  // phase 1 saved the (scaled) rows
+    const int k = idx >> 2, r = idx & 3;
+    xs[idx] = (r < valid && k < g.S) ? g.sv.xs[(size_t)k * g.sv.Bp + r0 + r] : 0.f;
   }
   __syncthreads();
-  // ---- updated critic at (s, mu): dhp2 = Wo * elu'(h')  (grad_ys = 1)   networks.py:143
-  sb_dense(xs, g.LX, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, nullptr, nullptr, 0, bufC,
-           g.LC, red);
-  sb_dense(mu, g.LX, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, nullptr, nullptr, 0,
-           bufC + g.CH1, g.LC, red);
-  sb_dense(bufC, g.LC, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_POST2, P + g.cWo,
-           nullptr, 0, bufD, g.LD, red);
-  // dca = dhp2 . Wh[CH1:]^T * elu'(ca), in place over ca (bufC[:, CH1:])
-  sb_dense(bufD, g.LD, g.CH2, GLB(g.whT) + g.CH1, 2 * g.CH1, g.CH1, nullptr, SB_AUX, nullptr,
-           bufC + g.CH1, g.LC, bufC + g.CH1, g.LC, red);
-  // da = dca . Wa^T -> dz3 (scratch), then dz3 = ((-da) * scale) * (1 - o^2), masked
-  sb_thin(bufC + g.CH1, g.LC, g.CH1, P + g.cWa, g.CH1, true, nullptr, g.A, dz3, g.LX, 0, red);
-  for (int idx = tid; idx < SB_R * g.A; idx += SB_NT) {
-    const int r = idx / g.A, a = idx - r * g.A;
-    const float ov = o[r * g.LX + a];
-    const float dy = __fmul_rn(-dz3[r * g.LX + a], g.scale);
-    dz3[r * g.LX + a] = r < valid ? __fmul_rn(dy, __fsub_rn(1.f, __fmul_rn(ov, ov))) : 0.f;
+  SB_STAMP(33);
+  {  // L1: actor h1 | critic state branch
+    const SbOp ops[2] = {sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1),
+                         sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat)};
+    const bool th[2] = {false, false};
+    sb_level<2>(ops, th, red);
+  }
+  SB_STAMP(34);
+  // L2: h2; L3: o = tanh(h2 W3), mu = scale o   (networks.py:51-63, ddpg.py:106)
+  sb_dense1(sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2), red);
+  SB_STAMP(35);
+  sb_thin1(sb_op(h2, g.AH2, P + g.aW3, g.A, g.A, nullptr, SB_NONE, o), false, true, red);
+  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) mu[idx] = __fmul_rn(o[idx], g.scale);
+  __syncthreads();
+  SB_STAMP(36);
+  // L4: action branch at mu; L5: dhp2 = Wo * elu'(h')  (updated critic, grad_ys = 1,
+  // networks.py:143); L6: dca = dhp2 . Wh[CH1:]^T * elu'(ca), in place over ca
+  sb_dense1(sb_op(mu, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, cat + 4 * g.CH1), red);
+  SB_STAMP(37);
+  sb_dense1(sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_POST2, dh, nullptr,
+                  P + g.cWo),
+            red);
+  SB_STAMP(38);
+  sb_dense1(sb_op(dh, g.CH2, GLB(g.whT) + g.CH1, 2 * g.CH1, g.CH1, nullptr, SB_AUX,
+                  cat + 4 * g.CH1, cat + 4 * g.CH1),
+            red);
+  SB_STAMP(39);
+  // L7: da = dca . Wa^T -> dz3 (scratch), then dz3 = ((-da) * scale) * (1 - o^2), masked
+  sb_thin1(sb_op(cat + 4 * g.CH1, g.CH1, P + g.cWa, g.CH1, g.A, nullptr, SB_NONE, dz3), true,
+           false, red);
+  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) {
+    const float ov = o[idx];
+    const float dy = __fmul_rn(-dz3[idx], g.scale);
+    dz3[idx] = (idx & 3) < valid ? __fmul_rn(dy, __fsub_rn(1.f, __fmul_rn(ov, ov))) : 0.f;
   }
   __syncthreads();
   // ---- actor backward (networks.py:44)
-  // dz2 = dz3 . W3^T * elu'(h2) -> bufD   (K = A is tiny: one thread per output)
-  for (int idx = tid; idx < SB_R * g.AH2; idx += SB_NT) {
-    const int r = idx / g.AH2, n = idx - r * g.AH2;
+  // dz2 = dz3 . W3^T * elu'(h2) -> dh   (K = A is tiny: one thread per output)
+  for (int idx = tid; idx < 4 * g.AH2; idx += SB_NT) {
+    const int n = idx >> 2, r = idx & 3;
     float v = 0.f;
-    for (int a = 0; a < g.A; ++a) v = fmaf(dz3[r * g.LX + a], P[g.aW3 + (size_t)n * g.A + a], v);
-    bufD[r * g.LD + n] = __fmul_rn(v, elu_grad_factor(bufB[r * g.LB + n]));
+    for (int a = 0; a < g.A; ++a) v = fmaf(dz3[a * 4 + r], P[g.aW3 + (size_t)n * g.A + a], v);
+    dh[idx] = __fmul_rn(v, elu_grad_factor(h2[idx]));
   }
   __syncthreads();
-  sb_wgrad(bufB, g.LB, g.AH2, dz3, g.LX, g.A, part + g.aW3, nullptr);
-  sb_wgrad(bufA, g.LA, g.AH1, bufD, g.LD, g.AH2, part + g.aW2, part + g.ab2);
-  __syncthreads();
-  // dz1 = dz2 . W2^T * elu'(h1), in place over h1 (bufA)
-  sb_dense(bufD, g.LD, g.AH2, GLB(g.w2T), g.AH1, g.AH1, nullptr, SB_AUX, nullptr, bufA, g.LA,
-           bufA, g.LA, red);
-  sb_wgrad(xs, g.LX, g.S, bufA, g.LA, g.AH1, part + g.aW1, part + g.ab1);
+  SB_STAMP(40);
+  // L8: dz1 = dz2 . W2^T * elu'(h1) -> cat
+  sb_dense1(sb_op(dh, g.AH2, GLB(g.w2T), g.AH1, g.AH1, nullptr, SB_AUX, cat, h1), red);
+  SB_STAMP(41);
+  sb_save(g.sv.h1, g.sv.Bp, g.AH1, h1, r0);
+  sb_save(g.sv.h2, g.sv.Bp, g.AH2, h2, r0);
+  sb_save(g.sv.dz1, g.sv.Bp, g.AH1, cat, r0);
+  sb_save(g.sv.dz2, g.sv.Bp, g.AH2, dh, r0);
+  sb_save(g.sv.dz3, g.sv.Bp, g.A, dz3, r0);
+  if (g.stamps) {
+    __syncthreads();
+    SB_STAMP(42);
+  }
 }
 
-// g = sum of the per-WG slabs (slab order); TF ApplyAdam with this step's
-// alpha; soft update of the target; transposed shadow of the dX weight
-// (critic Wh -> whT, actor W2 -> w2T).  net: 0 actor, 1 critic.  The critic
-// call also finalises the step stats.
-__global__ void sb_reduce_adam_kernel(SbArgs g, int net, int nslab) {
-  const long long b = net == 0 ? g.actor_begin : g.critic_begin;
-  const long long e = net == 0 ? g.actor_end : g.critic_end;
-  const long long sh_off = net == 0 ? g.aW2 : g.cWh;
-  const int sh_rows = net == 0 ? g.AH1 : 2 * g.CH1, sh_cols = net == 0 ? g.AH2 : g.CH2;
-  float* const sh = net == 0 ? g.w2T : g.whT;
-  const long long sh_n = (long long)sh_rows * sh_cols;
-  const float alpha = g.alpha[net];
-  const float omb1 = __fsub_rn(1.f, g.b1), omb2 = __fsub_rn(1.f, g.b2);
-  for (long long i = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < e;
-       i += (long long)gridDim.x * blockDim.x) {
-    float gv = 0.f;
-    for (int w = 0; w < nslab; ++w) gv += g.part[(size_t)w * g.PT + i];
-    float m = g.adam_m[i], v = g.adam_v[i], p = g.theta[i];
-    m = __fadd_rn(m, __fmul_rn(__fsub_rn(gv, m), omb1));
-    v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(gv, gv), v), omb2));
-    p = __fsub_rn(p, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), g.eps)));
+// One network's weight-gradient table: tensor i occupies param offsets
+// [off, off + K*N) (row-major [K][N]); its gradient is
+//   g[k][n] = sum_b X[k][b] dY[n][b]   (feature-major saves; X == nullptr: bias, X = 1)
+// over the B saved rows, computed by tiles of TK x TN elements (TK*TN = SB_GT)
+// starting at block tile0.
+struct SbGradT {
+  long long off;
+  int K, N;
+  const float* X;
+  int ldx;
+  const float* dY;
+  int ldy;
+  int TN, TK, tile0;
+};
+constexpr int SB_MAXT = 10;  // tensors per network + the sentinel
+struct SbGradTab {
+  SbGradT t[SB_MAXT];
+  int n;
+  int shadow;  // index of the tensor whose transpose is kept (Wh / W2), -1 none
+  float* sh;
+};
+
+// Weight gradients of one network over the whole batch (one ordered fp32
+// sum over b per element, no partial slabs), TF ApplyAdam with this step's
+// alpha, soft update of the target, and the transposed shadow of the dX
+// weight.  net: 0 actor, 1 critic; the critic call also finalises the step
+// stats.  Thread (k, n) reads column k of X and column n of dY straight from
+// global memory, SB_GU rows per batch with every load of a batch issued before
+// the first FMA (a wave shares k, so its X loads are one line and its dY
+// loads one contiguous run); the Adam state is loaded first so that its
+// round trip overlaps the gradient's.
+constexpr int SB_GU = 16;  // float4s (4 batch rows each) per batch of loads
+__global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTab tab, int net,
+                                                              int nslab) {
+  const int sbase = net == 1 ? 48 : 56;
+  SB_STAMP(sbase);
+  int ti = 0;
+#pragma unroll
+  for (int i = 1; i < SB_MAXT; ++i)
+    if (i < tab.n && (int)blockIdx.x >= tab.t[i].tile0) ti = i;
+  const SbGradT T = tab.t[ti];
+  const int local = blockIdx.x - T.tile0;
+  const int ntn = (T.N + T.TN - 1) / T.TN;
+  const int tid = threadIdx.x;
+  const int kl = tid / T.TN, nl = tid - kl * T.TN;
+  const int k = (local / ntn) * T.TK + kl, n = (local % ntn) * T.TN + nl;
+  const bool ok = k < T.K && n < T.N;
+  const int kc = min(k, T.K - 1), nc = min(n, T.N - 1);
+  const size_t i = (size_t)T.off + (size_t)kc * T.N + nc;
+  const float m0 = g.adam_m[i], v0 = g.adam_v[i], p0 = g.theta[i], t0 = g.target[i];
+  const f32x4* xp = T.X ? reinterpret_cast<const f32x4*>(T.X + (size_t)kc * T.ldx) : nullptr;
+  const f32x4* dp = reinterpret_cast<const f32x4*>(T.dY + (size_t)nc * T.ldy);
+  const int nq = (g.B + 3) >> 2;
+  float gv = 0.f;
+  for (int q0 = 0; q0 < nq; q0 += SB_GU) {
+    f32x4 xv[SB_GU], dv[SB_GU];
+#pragma unroll
+    for (int u = 0; u < SB_GU; ++u) {
+      const int qq = min(q0 + u, nq - 1);
+      xv[u] = xp ? xp[qq] : f32x4{1.f, 1.f, 1.f, 1.f};
+      dv[u] = dp[qq];
+    }
+#pragma unroll
+    for (int u = 0; u < SB_GU; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        gv = (4 * (q0 + u) + e < g.B) ? fmaf(xv[u][e], dv[u][e], gv) : gv;
+  }
+  SB_STAMP(sbase + 1);
+  if (ok) {
+    const float alpha = g.alpha[net];
+    const float omb1 = __fsub_rn(1.f, g.b1), omb2 = __fsub_rn(1.f, g.b2);
+    const float m = __fadd_rn(m0, __fmul_rn(__fsub_rn(gv, m0), omb1));
+    const float v = __fadd_rn(v0, __fmul_rn(__fsub_rn(__fmul_rn(gv, gv), v0), omb2));
+    const float p =
+        __fsub_rn(p0, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), g.eps)));
     g.adam_m[i] = m;
     g.adam_v[i] = v;
     g.theta[i] = p;
-    g.target[i] = __fadd_rn(__fmul_rn(p, g.tau), __fmul_rn(g.target[i], g.omt));
-    const long long si = i - sh_off;
-    if (si >= 0 && si < sh_n) {
-      const long long rr = si / sh_cols, cc = si - rr * sh_cols;
-      sh[cc * sh_rows + rr] = p;
-    }
+    g.target[i] = __fadd_rn(__fmul_rn(p, g.tau), __fmul_rn(t0, g.omt));
+    if (ti == tab.shadow) tab.sh[(size_t)n * T.K + k] = p;
   }
+  SB_STAMP(sbase + 2);
   if (net == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
     float ls = 0.f, qm = -INFINITY;
     for (int w = 0; w < nslab; ++w) {
