@@ -69,7 +69,7 @@ def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="
     fill_synthetic(rb, S, A, replay_rows, scale=scale, seed=seed)   # identical on every rank
     log("[bench] rank %d replay filled with %d rows in %.1fs" % (rank, replay_rows,
                                                                  time.time() - t0))
-    return sess, rb, FusedLearner(sess, rb, B * world)
+    return sess, rb, FusedLearner(sess, rb, B * world), actor
 
 
 def timed(fl, sess, steps, warmup, world):
@@ -125,6 +125,19 @@ def summarize_profile(rows, steps):
     gemm_flops = sum(r["flops"] for k, r in by_kernel.items() if k.startswith("gemm")) / steps
     dom = max(by_kernel.items(), key=lambda kv: kv[1]["ms"])
     return by_kernel, dom, gpu_ms, gemm_ms, gemm_flops
+
+
+def action_selection_latency(actor, S, calls=2000):
+    """actor.predict on one state (ddpg.py:68-70), host wall time per call
+    including the device round trip (states in, action out)."""
+    s = np.random.default_rng(0).standard_normal((1, S)).astype(np.float32)
+    for _ in range(50):
+        actor.predict(s)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        actor.predict(s)
+    el = time.perf_counter() - t0
+    return {"batch": 1, "us_per_call": round(1e6 * el / calls, 2), "calls": calls}
 
 
 def pmc_traffic(cfg_name, kernel):
@@ -220,7 +233,7 @@ def main():
     dtype = args.dtype or DEFAULT_DTYPE[cfg]
     S, A, H1, H2, B, scale, label = CONFIGS[cfg]
     label = "%s, %s GEMM operands (fp32 master weights/accumulation)" % (label, dtype)
-    sess, rb, fl = build_learner(cfg, local, rank, world, args.replay, dtype=dtype)
+    sess, rb, fl, _ = build_learner(cfg, local, rank, world, args.replay, dtype=dtype)
     el = timed(fl, sess, args.steps, args.warmup, world)
     ms = 1000.0 * el / args.steps
     value = world * args.steps / el   # batch-B updates processed by all ranks per second
@@ -273,7 +286,7 @@ def main():
     out["hbm_GBs"] = hbm
 
     if world == 1 and rank == 0 and not args.no_small and cfg != "c2":
-        s2, rb2, fl2 = build_learner("c2", local, 0, 1, 100_000)
+        s2, rb2, fl2, actor2 = build_learner("c2", local, 0, 1, 100_000)
         el2 = timed(fl2, s2, 500, 50, 1)
         rows2, wall2 = kernel_profile(fl2, s2, 100)
         busy2 = sum(r["ms"] for r in rows2.values()) / 100
@@ -282,7 +295,8 @@ def main():
             "workload": CONFIGS["c2"][6], "value": round(500 / el2, 1), "unit": "updates/s",
             "ms_per_step": round(1000 * el2 / 500, 4),
             "kernels_per_step": nk2, "gpu_busy_ms_per_step": round(busy2, 4),
-            "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1)}
+            "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1),
+            "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
         s2.close()
     if world == 1 and rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(cfg)

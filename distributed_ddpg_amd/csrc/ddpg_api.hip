@@ -195,6 +195,7 @@ struct ddpg_ctx {
   float* sb_w2T = nullptr;    // [AH2][AH1]   actor W2^T shadow
   bool sb_shadow_ok = false;  // cleared by every theta write outside the small path
   size_t sb_smem = 0;         // dynamic LDS bytes of the phase kernels
+  float* h_pred = nullptr;    // pinned [Bmax][A]: action-selection output (written by the GPU)
   int sb_xstride = 1;         // XCD packing of the phase kernels (env DDPG_SB_XCD=1: on)
   unsigned long long* sb_stamps = nullptr;  // diagnostic (env DDPG_SB_STAMPS=1)
 
@@ -801,9 +802,8 @@ static void sb_refresh_shadows(ddpg_ctx* c) {
   c->sb_shadow_ok = true;
 }
 
-// Small-batch learner step: 4 launches (small_batch.h); the gather from the
-// replay ring is fused into the phase kernels (slots already in c->d_slots).
-static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
+// Arguments of the small-batch kernels (rb may be null: action selection).
+static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   const Layout& L = c->L;
   SbArgs a;
   memset(&a, 0, sizeof a);
@@ -827,11 +827,13 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   a.lr_c = c->cfg.critic_lr;
   a.eps = c->cfg.epsilon;
   a.slots = c->d_slots;
-  a.rs = rb->rs;
-  a.ra = rb->ra;
-  a.rr = rb->rr;
-  a.rt = rb->rt;
-  a.rs2 = rb->rs2;
+  if (rb) {
+    a.rs = rb->rs;
+    a.ra = rb->ra;
+    a.rr = rb->rr;
+    a.rt = rb->rt;
+    a.rs2 = rb->rs2;
+  }
   a.mean = c->has_scaler ? c->dmean : nullptr;
   a.sdev = c->has_scaler ? c->dscale : nullptr;
   a.theta = c->theta;
@@ -861,6 +863,14 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   a.cbo = L.c[CBO].off;
   a.stamps = c->sb_stamps;
   a.xstride = c->sb_xstride;
+  return a;
+}
+
+// Small-batch learner step: 4 launches (small_batch.h); the gather from the
+// replay ring is fused into the phase kernels (slots already in c->d_slots).
+static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
+  const Layout& L = c->L;
+  const SbArgs a = sb_args(c, rb, B, inv_b);
   const int G = ceil_div(B, SB_R);
   const long long nc = (long long)(L.critic_end - L.critic_begin);
   const long long na = (long long)(L.actor_end - L.actor_begin);
@@ -955,6 +965,7 @@ static void ctx_free(ddpg_ctx* c) {
   for (int i = 0; i < kSlotRing; ++i)
     if (c->slot_ev[i]) (void)hipEventDestroy(c->slot_ev[i]);
   if (c->h_slots) (void)hipHostFree(c->h_slots);
+  if (c->h_pred) (void)hipHostFree(c->h_pred);
   for (auto& g : c->gslot) {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (g.h_idx) (void)hipHostFree(g.h_idx);
@@ -1211,6 +1222,9 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
         HIP_TRY(hipFuncSetAttribute((const void*)sb_phase3_kernel,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        HIP_TRY(hipFuncSetAttribute((const void*)sb_actor_predict_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+        HIP_TRY(hipHostMalloc(&c->h_pred, (size_t)c->Bmax * c->A * sizeof(float)));
         c->sb_ok = true;
         if (const char* st = getenv("DDPG_SB_STAMPS"))
           if (atoi(st)) {
@@ -1381,6 +1395,23 @@ int ddpg_set_scaler(ddpg_ctx* c, const double* mean, const double* scale, int S)
 int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_out) {
   return guard(c, [&] {
     check_b(c, B);
+    if (c->sb_ok && B * c->S <= SB_PRED_MAX) {
+      // action selection (ddpg.py:68-70): one launch, states in the kernel
+      // arguments, result written to pinned host memory
+      SbPredIn in;
+      memcpy(in.s, s, sizeof(float) * B * c->S);
+      const SbArgs a = sb_args(c, nullptr, B, 1.f);
+      const size_t smem = (SB_RED + 2 * SB_BIAS + 8 * (size_t)a.LX + 8 * (size_t)a.LW) * 4;
+      {
+        ProfScope ps(c, "sb_actor_predict", 0, 0);
+        hipLaunchKernelGGL(sb_actor_predict_kernel, dim3(ceil_div(B, SB_R)), dim3(SB_NT), smem,
+                           c->stream, a, target ? c->target : c->theta, in, c->h_pred);
+        HIP_TRY(hipGetLastError());
+      }
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      memcpy(a_out, c->h_pred, sizeof(float) * B * c->A);
+      return;
+    }
     upload_rows(c, c->s, c->ldS, s, B, c->S);
     apply_scaler(c, c->s, B);
     actor_fwd(c, target ? c->target : c->theta, c->s, B, c->h1, nullptr, nullptr, c->mu);

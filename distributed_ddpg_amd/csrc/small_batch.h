@@ -592,6 +592,47 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   }
 }
 
+// Action selection (ddpg.py:68-70, actor.predict at B = 1 .. 64): the whole
+// actor forward in one launch.  The states travel in the kernel arguments
+// (no upload), the scaler is applied in fp64 on device, and mu = scale *
+// tanh(elu(elu(s W1 + b1) W2 + b2) W3) is written straight to pinned host
+// memory (no download launch); one workgroup per 4 rows.
+constexpr int SB_PRED_MAX = 256;  // floats of state in the kernel arguments
+struct SbPredIn {
+  float s[SB_PRED_MAX];
+};
+__global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const float* base,
+                                                                 SbPredIn in, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * SB_R;
+  const int valid = min(SB_R, g.B - r0);
+  const int LX = g.LX, LW = g.LW;
+  lds_f* red = LDS(sm);
+  lds_f* xs = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
+  lds_f* o = xs + 4 * LX;
+  lds_f* h1 = o + 4 * LX;  // [LW][4]
+  lds_f* h2 = h1 + 4 * LW;
+  const glb_f* P = GLB(base);
+  for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
+    const int k = idx >> 2, r = idx & 3;
+    float x = 0.f;
+    if (r < valid && k < g.S) {
+      x = in.s[(r0 + r) * g.S + k];
+      if (g.mean) x = (float)(((double)x - g.mean[k]) / g.sdev[k]);
+    }
+    xs[idx] = x;
+  }
+  __syncthreads();
+  sb_dense1(sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1), red);
+  sb_dense1(sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2), red);
+  sb_thin1(sb_op(h2, g.AH2, P + g.aW3, g.A, g.A, nullptr, SB_NONE, o), false, true, red);
+  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) {
+    const int a = idx >> 2, r = idx & 3;
+    if (r < valid) out[(size_t)(r0 + r) * g.A + a] = __fmul_rn(o[idx], g.scale);
+  }
+}
+
 // One network's weight-gradient table: tensor i occupies param offsets
 // [off, off + K*N) (row-major [K][N]); its gradient is
 //   g[k][n] = sum_b X[k][b] dY[n][b]   (feature-major saves; X == nullptr: bias, X = 1)

@@ -486,3 +486,29 @@ def test_small_batch_path_matches_large_path(dd, O, monkeypatch, name):
     for x, y in zip(p1, p0):
         for u, v in zip(x, y):
             assert rel(u, v) < GRAD_TOL
+
+
+@pytest.mark.parametrize("name", ["ip", "odd"])
+def test_action_selection_single_launch(dd, O, name):
+    """actor.predict at B = 1 (ddpg.py:68-70, the action-selection forward,
+    SURVEY.md §8(f)1) is one sb_actor_predict launch (states in the kernel
+    arguments, result written to pinned host memory) and matches the oracle;
+    so is a small batch."""
+    from distributed_ddpg_amd.learner import Profile
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    sess, actor, critic = _session(dd, O, name, p)
+    s, _, _ = _batch(name)
+    prof = Profile(sess)
+    prof.enable(True)
+    for lo, hi in ((0, 1), (1, 2), (5, 6), (0, 9)):
+        for target, net in ((False, "actor"), (True, "actor_t")):
+            mu = actor.predict_target(s[lo:hi]) if target else actor.predict(s[lo:hi])
+            assert mu.dtype == np.float32 and mu.shape == (hi - lo, A)
+            ref = O.actor_forward(f64(p[net]), s[lo:hi].astype(np.float64), scale)[3]
+            assert rel(mu, ref) < FWD_TOL, (lo, hi, net)
+    keys = prof.read()
+    prof.enable(False)
+    assert any(k.startswith("sb_actor_predict") for k in keys), sorted(keys)
+    assert not any(k.startswith("gemm") for k in keys), sorted(keys)
+    sess.close()
