@@ -102,6 +102,7 @@ PROTOTYPES = [
     ("ddpg_comm_init", _c.c_int, [_P, _c.c_char_p, _c.c_int, _c.c_int]),
     ("ddpg_profile_enable", _c.c_int, [_P, _c.c_int]),
     ("ddpg_profile_read", _c.c_int, [_P, _c.c_int, _P, _dp, _i64p, _dp, _dp]),
+    ("ddpg_crc32c", _c.c_uint32, [_c.c_uint32, _c.c_void_p, _c.c_size_t]),
 ]
 
 for _name, _res, _args in PROTOTYPES:

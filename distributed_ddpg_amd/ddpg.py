@@ -97,7 +97,7 @@ def run_worker(opt, task_index, env_name, episodes, device):
     import torch.distributed as dist
     from torch.distributed import TCPStore
 
-    from . import networks as nets
+    from . import checkpoint, networks as nets, summary
     from .learner import FusedLearner, init_comm
     from .replay_buffer import ReplayBuffer
 
@@ -131,10 +131,19 @@ def run_worker(opt, task_index, env_name, episodes, device):
     sess.run(nets.global_variables_initializer(seed=opt.seed))
     actor.set_session(sess)
     critic.set_session(sess)
-    actor.update_target_network()   # ddpg.py:227-229
-    critic.update_target_network()
+    saver = checkpoint.Saver(max_to_keep=5)                     # ddpg.py:211
+    global_step = 0
+    latest = checkpoint.latest_checkpoint(opt.save_dir) if opt.continue_training else None
+    if latest:                                                   # ddpg.py:213-222
+        global_step = int(float(saver.restore(sess, latest)["global_step"]))
+        print("Model Restored from %s" % latest, flush=True)
+    else:
+        actor.update_target_network()   # ddpg.py:227-229
+        critic.update_target_network()
     init_comm(sess, rank, world)
     learner = FusedLearner(sess, replay, opt.batch_size)
+    is_chief = rank == 0
+    writer = summary.FileWriter(opt.summary_dir) if is_chief else None   # ddpg.py:241
 
     # Flat loop over environment steps: every rank performs exactly one
     # learner update per env step once warm, so the collectives inside the
@@ -158,13 +167,20 @@ def run_worker(opt, task_index, env_name, episodes, device):
         t += 1
         if done:
             stats.append(ep_reward)
-            if rank == 0:
+            if is_chief:  # ddpg.py:118-127
+                writer.add_episode(global_step, ep_reward, ep_q / max(t, 1), ep_loss / max(t, 1))
+                writer.flush()
                 print("Episode: %d - Iterations: %d - Reward: %f - Qmax: %f - Loss: %f" % (
-                    episode, t, ep_reward, ep_q / max(t, 1), ep_loss / max(t, 1)), flush=True)
-            if np.mean(stats[-100:]) > 950 and len(stats) >= 101:  # ddpg.py:255
+                    global_step, t, ep_reward, ep_q / max(t, 1), ep_loss / max(t, 1)), flush=True)
+            if np.mean(stats[-100:]) > 950 and len(stats) >= 101:  # ddpg.py:255-260
                 print(np.mean(stats[-100:]))
                 print("Solved.")
                 solved = True
+                if is_chief:
+                    saver.save(sess, opt.save_dir + "/model", global_step=global_step)
+            elif is_chief and episode % opt.valid_freq == opt.valid_freq - 1:  # ddpg.py:262-264
+                saver.save(sess, opt.save_dir + "/model", global_step=global_step)
+            global_step += 1  # ddpg.py:267 step_op
             episode += 1
             t = 0
             ep_reward, ep_q, ep_loss = 0.0, 0.0, 0.0
@@ -176,6 +192,8 @@ def run_worker(opt, task_index, env_name, episodes, device):
             stop = bool(flag.item())
         if stop:
             break
+    if writer:
+        writer.close()
     sess.close()
     if world > 1:
         dist.destroy_process_group()

@@ -188,6 +188,13 @@ int ddpg_profile_enable(ddpg_ctx* ctx, int enable);
 int ddpg_profile_read(ddpg_ctx* ctx, int n, char (*names)[64], double* ms, int64_t* launches,
                       double* flops, double* bytes);
 
+/* ------------------------------------------------------------- checkpoints */
+/* CRC-32C (Castagnoli) of n bytes continuing from crc (0 to start): the checksum
+ * of TF V2 checkpoint blocks and tensors, for the tf.train.Saver work-alike
+ * (distributed_ddpg_amd/checkpoint.py; replaces TF's Saver.save/restore,
+ * ddpg.py:155-159, 211-222).  Host only, thread-safe. */
+uint32_t ddpg_crc32c(uint32_t crc, const void* data, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -512,3 +512,81 @@ def test_action_selection_single_launch(dd, O, name):
     assert any(k.startswith("sb_actor_predict") for k in keys), sorted(keys)
     assert not any(k.startswith("gemm") for k in keys), sorted(keys)
     sess.close()
+
+
+def test_saver_restores_reference_checkpoint_and_resumes(dd, O, tmp_path):
+    """tf.train.Saver work-alike on a live session: restore
+    the reference's MountainCar model-120 (ddpg.py:213-222), check every
+    tensor and both beta-power pairs on the device, continue training one
+    fused step from it (non-trivial Adam bias correction, t ~ 45k), and
+    check that saving the untouched restored state reproduces TF's bytes."""
+    from distributed_ddpg_amd import _lib, checkpoint as C
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    ref = os.path.join(GOLD, "ckpt", "model-120")
+    p, _ = _params(O, "mc")
+    sess, actor, critic = _session(dd, O, "mc", p)
+    saver = C.Saver()
+    t = saver.restore(sess, ref)
+    for which, names in ((_lib.ACTOR, C.ACTOR), (_lib.CRITIC, C.CRITIC),
+                         (_lib.ACTOR_TARGET, C.ACTOR_TARGET), (_lib.CRITIC_TARGET, C.CRITIC_TARGET),
+                         (_lib.ACTOR_ADAM_V, [n + "/Adam_1" for n in C.ACTOR]),
+                         (_lib.CRITIC_ADAM_M, [n + "/Adam" for n in C.CRITIC])):
+        for n, v in zip(names, sess.get_params(which)):
+            np.testing.assert_array_equal(v, t[n].reshape(v.shape))
+    assert sess.get_adam_powers(1) == (float(t["beta1_power_1"]), float(t["beta2_power_1"]))
+    out = saver.save(sess, str(tmp_path / "model"), global_step=120,
+                     summary_values=[float(t[v]) for v in C.SUMMARY_VARS])
+    for ext in (".index", ".data-00000-of-00001"):
+        assert open(out + ext, "rb").read() == open(ref + ext, "rb").read(), ext
+    # resume: one fused learner step from the restored state vs the oracle
+    import random
+    rb = ReplayBuffer(2000, 1234)
+    rows = _fill(rb, 2, 1, 1000, 1.0, seed=4)
+    L = O.Learner(2, 1, 48, 64, 1.0, dtype=np.float64, init_blend=False, CH1=48, CH2=128,
+                  params={"actor": dict(zip(O.ACTOR_KEYS, [t[n] for n in C.ACTOR])),
+                          "actor_t": dict(zip(O.ACTOR_KEYS, [t[n] for n in C.ACTOR_TARGET])),
+                          "critic": dict(zip(O.CRITIC_KEYS, [t[n] for n in C.CRITIC])),
+                          "critic_t": dict(zip(O.CRITIC_KEYS, [t[n] for n in C.CRITIC_TARGET]))})
+    for opt, keys, names, sfx in ((L.actor_opt, O.ACTOR_KEYS, C.ACTOR, ""),
+                                  (L.critic_opt, O.CRITIC_KEYS, C.CRITIC, "_1")):
+        for k, n in zip(keys, names):
+            opt.m[k] = t[n + "/Adam"].astype(np.float64)
+            opt.v[k] = t[n + "/Adam_1"].astype(np.float64)
+        opt.b1p = np.float64(t["beta1_power" + sfx])
+        opt.b2p = np.float64(t["beta2_power" + sfx])
+    idx = np.array(random.Random(1234).sample(range(1000), 64))
+    FusedLearner(sess, rb, 64).step()
+    L.step(*(x[idx] for x in rows))
+    for which, net, names in ((_lib.ACTOR, "actor", O.ACTOR_KEYS),
+                              (_lib.CRITIC, "critic", O.CRITIC_KEYS)):
+        for k, v in zip(names, sess.get_params(which)):
+            assert rel(v, L.state()[net][k].reshape(v.shape)) < GRAD_TOL, (net, k)
+    sess.close()
+
+
+def test_worker_driver_summaries_and_checkpoints(tmp_path):
+    """The ddpg.py-compatible worker (episode loop on the fused path) writes
+    the chief's TensorBoard scalars every episode (ddpg.py:118-125) and a
+    checkpoint every valid_freq episodes (ddpg.py:262-264); continue_training
+    restores the latest one (ddpg.py:213-222) and resumes its global_step."""
+    from distributed_ddpg_amd import checkpoint as C, ddpg, summary as Sm
+    from distributed_ddpg_amd.parameters import Parameters
+    opt = Parameters()
+    opt.batch_size, opt.rm_size, opt.valid_freq = 64, 20000, 2
+    opt.summary_dir, opt.save_dir = str(tmp_path / "tboard"), str(tmp_path / "model")
+    ddpg.run_worker(opt, 0, "synthetic", 3, 0)
+    ev = [f for f in os.listdir(opt.summary_dir) if f.startswith("events.out.tfevents.")]
+    assert len(ev) == 1
+    sc = Sm.read_scalars(os.path.join(opt.summary_dir, ev[0]))
+    assert [s for s, _ in sc["Reward"]] == [0, 1, 2]
+    assert all(v >= 1.0 for _, v in sc["Reward"]) and len(sc["Value_Loss"]) == 3
+    latest = C.latest_checkpoint(opt.save_dir)
+    assert latest.endswith("model-1")
+    t = C.read_bundle(latest)
+    assert float(t["global_step"]) == 1.0 and len(t) == 62
+    opt.continue_training = True
+    opt.summary_dir = str(tmp_path / "tboard2")
+    ddpg.run_worker(opt, 0, "synthetic", 1, 0)
+    ev2 = os.listdir(opt.summary_dir)[0]
+    assert [s for s, _ in Sm.read_scalars(os.path.join(opt.summary_dir, ev2))["Reward"]] == [1]
