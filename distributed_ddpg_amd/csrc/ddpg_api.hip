@@ -16,6 +16,7 @@
 #include "../../include/ddpg_hip.h"
 #include "gemm_f32.h"
 #include "gemm_bf16.h"
+#include "gemm_s3.h"
 #include "kernels.h"
 #include "sampler.h"
 #include "small_batch.h"
@@ -342,6 +343,7 @@ static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const Ge
 }
 
 static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec);
+static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec);
 
 template <int AL, int BL>
 static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
@@ -353,7 +355,8 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   const bool vb = (contB % 4 == 0) && (ldb % 4 == 0) && aligned16(B);
   const bool vec = va && vb;
   const bool bf = use_bf16(c, M, N, vec);
-  GemmPlan p = make_plan(M, N, K, splits, cap, bf);
+  const bool s3 = !bf && use_s3(c, M, N, vec);
+  GemmPlan p = make_plan(M, N, K, splits, cap, bf || s3);
   if (M <= 0 || N <= 0) return p;
   GemmArgs g;
   g.A = A;
@@ -372,6 +375,8 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   char key[112];
   if (bf)
     snprintf(key, sizeof key, "gemm_bf16_kernel<%s,%s>|%s", lay[AL], lay[BL], name);
+  else if (s3)
+    snprintf(key, sizeof key, "gemm_s3_kernel<%s,%s>|%s", lay[AL], lay[BL], name);
   else
     snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d,%d,%d,%d>|%s", lay[AL], lay[BL],
              va ? 4 : 1, vb ? 4 : 1, p.bm, p.bn, name);
@@ -380,6 +385,8 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
                4.0 * ((double)M * K + (double)K * N + (double)M * N * p.splits));
   if (bf)
     hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), grid, dim3(GNT), 0, c->cur, g);
+  else if (s3)
+    hipLaunchKernelGGL((gemm_s3_kernel<AL, BL>), grid, dim3(S3_NT), 0, c->cur, g);
   else if (va && vb)
     gemm_dispatch<AL, BL, 4, 4>(p, grid, c->cur, g);
   else if (va)
@@ -396,6 +403,18 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
 // shapes stay on the exact-fp32 kernel)
 static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec) {
   return c->cfg.dtype == DDPG_BF16 && vec && M >= 128 && N >= 128;
+}
+
+// fp32 contexts: the large GEMMs run fp32-accurate on the bf16 pipe
+// (gemm_s3.h, three-plane split); env DDPG_GEMM=f32 keeps every GEMM on the
+// fp32-input MFMA kernel.
+static int g_gemm_s3 = -1;
+static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec) {
+  if (g_gemm_s3 < 0) {
+    const char* v = getenv("DDPG_GEMM");
+    g_gemm_s3 = !(v && strcmp(v, "f32") == 0);
+  }
+  return g_gemm_s3 && c->cfg.dtype == DDPG_FP32 && vec && M >= 128 && N >= 128;
 }
 
 // ====================================================================== building blocks

@@ -42,7 +42,7 @@ template <int BM, int BN>
 struct TileCfg {
   static constexpr int STAGE = 2 * GBK * (BM + 1) + 2 * GBK * (BN + 1);
   static constexpr int VS_LD = BN + 4;
-  static constexpr int EPI = (BM / 2) * VS_LD + BN * PROJ_MAX + GNT;
+  static constexpr int EPI = (BM / 2) * VS_LD + BN * PROJ_MAX + 2 * GNT;  // red: up to 512 threads
   static constexpr int SMEM = STAGE > EPI ? STAGE : EPI;
 };
 
@@ -98,14 +98,18 @@ DDPG_DEV void xcd_tile(int& bx, int& by, int on) {
   bx = wgid - by * nx;
 }
 
-template <int BM, int BN>
-DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / 64], float* smem, const GemmArgs& g,
+// WGN: waves along N (2 for the 4-wave kernels, 4 for the 8-wave gemm_s3);
+// the block always has 2 waves along M, each owning BM/2 rows.
+template <int BM, int BN, int WGN = 2>
+DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem,
+                            const GemmArgs& g,
                             int tid, int n0, int m0, int z, int bx, int by) {
   using TC = TileCfg<BM, BN>;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int WR = BM / 2, WC = BN / 2;
+  constexpr int NT = 2 * WGN * 64;  // threads
+  constexpr int TM = BM / 64, TN = BN / (32 * WGN);
+  constexpr int WR = BM / 2, WC = BN / WGN;
   const int wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int h = lane >> 5, li = lane & 31;
   const GemmEpi& e = g.e;
   const int M = g.M, N = g.N;
@@ -142,16 +146,16 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / 64], float* smem, const 
   constexpr int VS_LD = TC::VS_LD;
   float* Vs = smem;                      // [WR][VS_LD]
   float* Wps = smem + WR * VS_LD;        // [BN][PN]
-  float* red = Wps + BN * PROJ_MAX;      // [GNT]
+  float* red = Wps + BN * PROJ_MAX;      // [NT]
   const int PN = (e.proj_n + 3) & ~3;
   if (e.proj_out) {
-    for (int idx = tid; idx < BN * PN; idx += GNT) {
+    for (int idx = tid; idx < BN * PN; idx += NT) {
       const int nl = idx / PN, a = idx - nl * PN, n = n0 + nl;
       Wps[idx] = (n < N && a < e.proj_n) ? e.proj[(size_t)n * e.proj_sn + (size_t)a * e.proj_sa]
                                           : 0.f;
     }
   }
-  constexpr int CG = GNT / BN;  // column-sum row groups
+  constexpr int CG = NT / BN;  // column-sum row groups
   float csum = 0.f;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
@@ -174,7 +178,7 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / 64], float* smem, const 
     }
     if (e.proj_out) {
       const int PG = PN >> 2;
-      for (int p = tid; p < WR * PG; p += GNT) {
+      for (int p = tid; p < WR * PG; p += NT) {
         const int row = p % WR, ag = p / WR;
         float4 ap = make_float4(0.f, 0.f, 0.f, 0.f);
         // partial unroll: a full unroll makes every Wps load invariant in p

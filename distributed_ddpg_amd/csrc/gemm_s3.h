@@ -1,0 +1,199 @@
+// fp32-accurate GEMM on the bf16 MFMA pipe (gfx950, v_mfma_f32_32x32x16_bf16):
+// every fp32 operand x is split exactly into three bf16 planes
+//   h = bf16(x),  m = bf16(x - h),  l = bf16(x - h - m)      (x = h + m + l + O(2^-27 |x|))
+// (both differences are exact in fp32), and each product is the sum of the
+// six plane products that reach fp32 precision,
+//   x y ~ hh + hm + mh + hl + mm + lh                         (dropped: O(2^-27 |x y|)),
+// each an exact 8x8-bit product accumulated in fp32 by the MFMA.  The result
+// is an fp32 GEMM whose per-product error is below fp32 rounding (2^-24);
+// only the accumulation order differs from the fp32-input MFMA (both are fp32
+// sums).  The bf16 pipe's dense rate is 16x the fp32 one, so six bf16 MFMAs
+// per fp32 MAC group still run at up to 16/6 = 2.7x the fp32 MFMA peak.
+//
+// Tile 128 x 128 x 32, 512 threads = 8 waves (2 along M x 4 along N), each
+// wave 64 x 32 = 2 MFMA 32x32 tiles, two 16-deep k-steps per k-tile; 1 block
+// per CU (LDS: 3 planes x 2 operands x 2 stages), 2 waves per SIMD.  The split happens while staging (fp32
+// global -> registers -> split -> three bf16 LDS planes, [row][k] with 40-bf16
+// rows as in gemm_bf16.h), so the operands stay fp32 in HBM and every epilogue
+// of gemm_common.h applies unchanged.
+#pragma once
+#include "gemm_bf16.h"
+
+namespace ddpg {
+
+constexpr int S3_PLANE = 128 * H_ROW;                  // bf16 per plane (one operand, one stage)
+constexpr int S3_STAGE = 3 * S3_PLANE;                 // one operand, one stage
+constexpr int S3_SMEM_HALFS = 2 * 2 * S3_STAGE;        // 2 operands x 2 stages
+constexpr int S3_SMEM = (S3_SMEM_HALFS / 2 > TileCfg<128, 128>::EPI) ? S3_SMEM_HALFS / 2
+                                                                     : TileCfg<128, 128>::EPI;
+
+// x -> (h, m, l) bf16 planes, round-to-nearest-even each time (v_cvt_pk_bf16_f32).
+DDPG_DEV void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+#ifdef S3_TIMING_NOSPLIT  // tuning experiment only: wrong results
+  h = m = l = (__bf16)x;
+  return;
+#endif
+  h = (__bf16)x;
+  const float r1 = __fsub_rn(x, (float)h);
+  m = (__bf16)r1;
+  const float r2 = __fsub_rn(r1, (float)m);
+  l = (__bf16)r2;
+}
+
+constexpr int S3_NT = 512;  // 8 waves: 2 along M x 4 along N, wave tile 64 x 32
+
+// 128 rows x 32 k of fp32 for S3_NT threads, 8 floats each.
+//   RK (rows contiguous in k): float4 f = i*512 + tid -> row f>>3, k quad f&7.
+//   KR (k-major): thread (k pair kp = tid&15, row quad rq = tid>>4) loads rows
+//   4rq..4rq+3 of k = 2kp, 2kp+1 (each wave reads 16 k-rows x 64 B), and the
+//   transposed bf16x2 stores of a wave cover all 64 LDS banks.
+template <int L>
+struct StageS3 {
+  float v[8];
+
+  DDPG_DEV void load(const float* __restrict__ P, int ld, int R, int kend, int r0, int k0,
+                     int tid) {
+    if constexpr (L == L_RK) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int f = i * S3_NT + tid, r = f >> 3, kq = f & 7;
+        const int gr = r0 + r, gk = k0 + 4 * kq;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gr < R && gk < kend) x = *reinterpret_cast<const float4*>(P + (size_t)gr * ld + gk);
+        v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+      }
+    } else {
+      const int kp = tid & 15, rq = tid >> 4;
+      const int gr = r0 + 4 * rq;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int gk = k0 + 2 * kp + j;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gk < kend && gr < R) x = *reinterpret_cast<const float4*>(P + (size_t)gk * ld + gr);
+        v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
+      }
+    }
+  }
+
+  // split into the three bf16 planes [row][H_ROW] of one stage
+  DDPG_DEV void store(__bf16* __restrict__ lds, int tid) const {
+    __bf16 hm[3][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) split3(v[i], hm[0][i], hm[1][i], hm[2][i]);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      __bf16* pl = lds + p * S3_PLANE;
+      if constexpr (L == L_RK) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int f = i * S3_NT + tid, r = f >> 3, kq = f & 7;
+          bf16x4 q;
+          q[0] = hm[p][4 * i];
+          q[1] = hm[p][4 * i + 1];
+          q[2] = hm[p][4 * i + 2];
+          q[3] = hm[p][4 * i + 3];
+          *reinterpret_cast<bf16x4*>(pl + r * H_ROW + 4 * kq) = q;
+        }
+      } else {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const int kp = tid & 15, rq = tid >> 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // row 4rq+i gets k = 2kp, 2kp+1
+          bf16x2 q;
+          q[0] = hm[p][i];
+          q[1] = hm[p][4 + i];
+          *reinterpret_cast<bf16x2*>(pl + (4 * rq + i) * H_ROW + 2 * kp) = q;
+        }
+      }
+    }
+  }
+};
+
+template <int AL, int BL>
+__global__ __launch_bounds__(S3_NT, 1) void gemm_s3_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float smem[S3_SMEM];
+  __bf16* const As0 = reinterpret_cast<__bf16*>(smem);   // [stage][plane][128][H_ROW]
+  __bf16* const Bs0 = As0 + 2 * S3_STAGE;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int h = lane >> 5, li = lane & 31;
+  int bx, by;
+  xcd_tile(bx, by, g.xcd);
+  const int n0 = bx * H_BN, m0 = by * H_BM, z = blockIdx.z;
+  const int kbeg = z * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nk = kend > kbeg ? (kend - kbeg + GBK - 1) / GBK : 0;
+
+  f32x16 acc[2][1];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+
+  // k-tile t lives in LDS stage t & 1.  Registers hold the fp32 loads of the
+  // next two k-tiles (sets 0 and 1, alternating): tile t+1's split + LDS
+  // store and tile t+2's global loads are issued before tile t's MFMAs, and
+  // with two waves per SIMD one wave's MFMAs overlap the other's LDS reads
+  // and split VALU work.  Loads past kend read zeros.
+  auto mfma_tile = [&](const __bf16* As, const __bf16* Bs) {
+    const __bf16* a_s = As + (wm * 64 + li) * H_ROW + 8 * h;
+    const __bf16* b_s = Bs + (wn * 32 + li) * H_ROW + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < GBK / 16; ++ks) {
+      bf16x8 av[3][2], bv[3];  // [plane][tile]
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          av[p][i] =
+              *reinterpret_cast<const bf16x8*>(a_s + p * S3_PLANE + i * 32 * H_ROW + ks * 16);
+        bv[p] = *reinterpret_cast<const bf16x8*>(b_s + p * S3_PLANE + ks * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // small terms first: lh, mm, hl, mh, hm, hh  (planes 0 = h, 1 = m, 2 = l)
+        f32x16 c = acc[i][0];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], c, 0, 0, 0);
+        acc[i][0] = c;
+      }
+    }
+  };
+  if (nk > 0) {
+    StageS3<AL> sa0, sa1;
+    StageS3<BL> sb0, sb1;
+    __bf16* const A1 = As0 + S3_STAGE;
+    __bf16* const B1 = Bs0 + S3_STAGE;
+    sa0.load(g.A, g.lda, g.M, kend, m0, kbeg, tid);
+    sb0.load(g.B, g.ldb, g.N, kend, n0, kbeg, tid);
+    sa1.load(g.A, g.lda, g.M, kend, m0, kbeg + GBK, tid);
+    sb1.load(g.B, g.ldb, g.N, kend, n0, kbeg + GBK, tid);
+    sa0.store(As0, tid);
+    sb0.store(Bs0, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; t += 2) {
+      sa1.store(A1, tid);
+      sb1.store(B1, tid);
+      sa0.load(g.A, g.lda, g.M, kend, m0, kbeg + (t + 2) * GBK, tid);
+      sb0.load(g.B, g.ldb, g.N, kend, n0, kbeg + (t + 2) * GBK, tid);
+      mfma_tile(As0, Bs0);
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      sa0.store(As0, tid);
+      sb0.store(Bs0, tid);
+      sa1.load(g.A, g.lda, g.M, kend, m0, kbeg + (t + 3) * GBK, tid);
+      sb1.load(g.B, g.ldb, g.N, kend, n0, kbeg + (t + 3) * GBK, tid);
+      mfma_tile(A1, B1);
+      __syncthreads();
+    }
+  }
+  gemm_epilogue<128, 128, 4>(acc, smem, g, tid, n0, m0, z, bx, by);
+}
+
+}  // namespace ddpg
