@@ -27,83 +27,107 @@ constexpr int S3_SMEM_HALFS = 2 * 2 * S3_STAGE;        // 2 operands x 2 stages
 constexpr int S3_SMEM = (S3_SMEM_HALFS / 2 > TileCfg<128, 128>::EPI) ? S3_SMEM_HALFS / 2
                                                                      : TileCfg<128, 128>::EPI;
 
-// x -> (h, m, l) bf16 planes, round-to-nearest-even each time (v_cvt_pk_bf16_f32).
-DDPG_DEV void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+constexpr int S3_NT = 512;  // 8 waves: 2 along M x 4 along N, wave tile 64 x 32
+
+// (x0, x1) -> packed (h, m, l) bf16 pairs: three v_cvt_pk_bf16_f32, the
+// widening of a bf16 pair is two bit operations, the residuals packed f32 subs.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+DDPG_DEV f32x2v widen(bf16x2 b) {
+  const unsigned u = __builtin_bit_cast(unsigned, b);
+  return f32x2v{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xFFFF0000u)};
+}
+DDPG_DEV void split3_pair(f32x2v x, bf16x2& h, bf16x2& m, bf16x2& l) {
 #ifdef S3_TIMING_NOSPLIT  // tuning experiment only: wrong results
-  h = m = l = (__bf16)x;
+  h = m = l = __builtin_convertvector(x, bf16x2);
   return;
 #endif
-  h = (__bf16)x;
-  const float r1 = __fsub_rn(x, (float)h);
-  m = (__bf16)r1;
-  const float r2 = __fsub_rn(r1, (float)m);
-  l = (__bf16)r2;
+  h = __builtin_convertvector(x, bf16x2);
+  const f32x2v r1 = x - widen(h);  // exact
+  m = __builtin_convertvector(r1, bf16x2);
+  const f32x2v r2 = r1 - widen(m);  // exact
+  l = __builtin_convertvector(r2, bf16x2);
 }
-
-constexpr int S3_NT = 512;  // 8 waves: 2 along M x 4 along N, wave tile 64 x 32
 
 // 128 rows x 32 k of fp32 for S3_NT threads, 8 floats each.
 //   RK (rows contiguous in k): float4 f = i*512 + tid -> row f>>3, k quad f&7.
 //   KR (k-major): thread (k pair kp = tid&15, row quad rq = tid>>4) loads rows
 //   4rq..4rq+3 of k = 2kp, 2kp+1 (each wave reads 16 k-rows x 64 B), and the
 //   transposed bf16x2 stores of a wave cover all 64 LDS banks.
+// Per-thread pointers are set once and advanced one k-tile per load; rows out
+// of range read a clamped address and are zeroed (no branches), and only a
+// partial last k-tile checks k.
 template <int L>
 struct StageS3 {
   float v[8];
+  const float* p[2];
+  const float* base;  // 16-B aligned matrix start: the address of masked loads
+  bool rok[2];
+  int kof[2];    // k offset of each load within the k-tile
+  long long step;  // floats between consecutive k-tiles
 
-  DDPG_DEV void load(const float* __restrict__ P, int ld, int R, int kend, int r0, int k0,
-                     int tid) {
+  DDPG_DEV void init(const float* __restrict__ P, int ld, int R, int r0, int kbeg, int tid) {
+    base = P;
     if constexpr (L == L_RK) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int f = i * S3_NT + tid, r = f >> 3, kq = f & 7;
-        const int gr = r0 + r, gk = k0 + 4 * kq;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gr < R && gk < kend) x = *reinterpret_cast<const float4*>(P + (size_t)gr * ld + gk);
-        v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+        rok[i] = r0 + r < R;
+        p[i] = P + (size_t)(rok[i] ? r0 + r : 0) * ld + kbeg + 4 * kq;
+        kof[i] = 4 * kq;
       }
+      step = GBK;
     } else {
       const int kp = tid & 15, rq = tid >> 4;
-      const int gr = r0 + 4 * rq;
+      const bool ok = r0 + 4 * rq < R;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int gk = k0 + 2 * kp + j;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gk < kend && gr < R) x = *reinterpret_cast<const float4*>(P + (size_t)gk * ld + gr);
-        v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
+        rok[j] = ok;
+        p[j] = P + (size_t)(kbeg + 2 * kp + j) * ld + (ok ? r0 + 4 * rq : 0);
+        kof[j] = 2 * kp + j;
       }
+      step = (long long)GBK * ld;
+    }
+  }
+
+  // k-tile t; krem = k extent left from this tile's start (>= GBK: full tile)
+  DDPG_DEV void load(int t, int krem) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = rok[i] && (krem >= GBK || kof[i] < krem);
+      const float* q = ok ? p[i] + t * step : base;
+      const float4 x = *reinterpret_cast<const float4*>(q);
+      v[4 * i] = ok ? x.x : 0.f;
+      v[4 * i + 1] = ok ? x.y : 0.f;
+      v[4 * i + 2] = ok ? x.z : 0.f;
+      v[4 * i + 3] = ok ? x.w : 0.f;
     }
   }
 
   // split into the three bf16 planes [row][H_ROW] of one stage
   DDPG_DEV void store(__bf16* __restrict__ lds, int tid) const {
-    __bf16 hm[3][8];
+    if constexpr (L == L_RK) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) split3(v[i], hm[0][i], hm[1][i], hm[2][i]);
+      for (int i = 0; i < 2; ++i) {
+        const int f = i * S3_NT + tid, r = f >> 3, kq = f & 7;
+        bf16x2 h0, m0, l0, h1, m1, l1;
+        split3_pair(f32x2v{v[4 * i], v[4 * i + 1]}, h0, m0, l0);
+        split3_pair(f32x2v{v[4 * i + 2], v[4 * i + 3]}, h1, m1, l1);
+        __bf16* q = lds + r * H_ROW + 4 * kq;
+        *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<bf16x4*>(q + S3_PLANE) = bf16x4{m0[0], m0[1], m1[0], m1[1]};
+        *reinterpret_cast<bf16x4*>(q + 2 * S3_PLANE) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+      }
+    } else {
+      const int kp = tid & 15, rq = tid >> 4;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      __bf16* pl = lds + p * S3_PLANE;
-      if constexpr (L == L_RK) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int f = i * S3_NT + tid, r = f >> 3, kq = f & 7;
-          bf16x4 q;
-          q[0] = hm[p][4 * i];
-          q[1] = hm[p][4 * i + 1];
-          q[2] = hm[p][4 * i + 2];
-          q[3] = hm[p][4 * i + 3];
-          *reinterpret_cast<bf16x4*>(pl + r * H_ROW + 4 * kq) = q;
-        }
-      } else {
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        const int kp = tid & 15, rq = tid >> 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {  // row 4rq+i gets k = 2kp, 2kp+1
-          bf16x2 q;
-          q[0] = hm[p][i];
-          q[1] = hm[p][4 + i];
-          *reinterpret_cast<bf16x2*>(pl + (4 * rq + i) * H_ROW + 2 * kp) = q;
-        }
+      for (int i = 0; i < 4; ++i) {  // row 4rq+i gets k = 2kp, 2kp+1
+        bf16x2 hh, mm, ll;
+        split3_pair(f32x2v{v[i], v[4 + i]}, hh, mm, ll);
+        __bf16* q = lds + (4 * rq + i) * H_ROW + 2 * kp;
+        *reinterpret_cast<bf16x2*>(q) = hh;
+        *reinterpret_cast<bf16x2*>(q + S3_PLANE) = mm;
+        *reinterpret_cast<bf16x2*>(q + 2 * S3_PLANE) = ll;
       }
     }
   }
@@ -168,27 +192,32 @@ __global__ __launch_bounds__(S3_NT, 1) void gemm_s3_kernel(GemmArgs g) {
   if (nk > 0) {
     StageS3<AL> sa0, sa1;
     StageS3<BL> sb0, sb1;
+    sa0.init(g.A, g.lda, g.M, m0, kbeg, tid);
+    sb0.init(g.B, g.ldb, g.N, n0, kbeg, tid);
+    sa1 = sa0;
+    sb1 = sb0;
+    const int klen = kend - kbeg;
     __bf16* const A1 = As0 + S3_STAGE;
     __bf16* const B1 = Bs0 + S3_STAGE;
-    sa0.load(g.A, g.lda, g.M, kend, m0, kbeg, tid);
-    sb0.load(g.B, g.ldb, g.N, kend, n0, kbeg, tid);
-    sa1.load(g.A, g.lda, g.M, kend, m0, kbeg + GBK, tid);
-    sb1.load(g.B, g.ldb, g.N, kend, n0, kbeg + GBK, tid);
+    sa0.load(0, klen);
+    sb0.load(0, klen);
+    sa1.load(1, klen - GBK);
+    sb1.load(1, klen - GBK);
     sa0.store(As0, tid);
     sb0.store(Bs0, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
       sa1.store(A1, tid);
       sb1.store(B1, tid);
-      sa0.load(g.A, g.lda, g.M, kend, m0, kbeg + (t + 2) * GBK, tid);
-      sb0.load(g.B, g.ldb, g.N, kend, n0, kbeg + (t + 2) * GBK, tid);
+      sa0.load(t + 2, klen - (t + 2) * GBK);
+      sb0.load(t + 2, klen - (t + 2) * GBK);
       mfma_tile(As0, Bs0);
       __syncthreads();
       if (t + 1 >= nk) break;
       sa0.store(As0, tid);
       sb0.store(Bs0, tid);
-      sa1.load(g.A, g.lda, g.M, kend, m0, kbeg + (t + 3) * GBK, tid);
-      sb1.load(g.B, g.ldb, g.N, kend, n0, kbeg + (t + 3) * GBK, tid);
+      sa1.load(t + 3, klen - (t + 3) * GBK);
+      sb1.load(t + 3, klen - (t + 3) * GBK);
       mfma_tile(A1, B1);
       __syncthreads();
     }
