@@ -384,9 +384,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   ProfScope ps(c, key, 2.0 * M * N * (double)K,
                4.0 * ((double)M * K + (double)K * N + (double)M * N * p.splits));
   if (bf)
-    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), grid, dim3(GNT), 0, c->cur, g);
+    hipLaunchKernelGGL((gemm_s3_kernel<AL, BL, 1>), grid, dim3(S3_NT), 0, c->cur, g);
   else if (s3)
-    hipLaunchKernelGGL((gemm_s3_kernel<AL, BL>), grid, dim3(S3_NT), 0, c->cur, g);
+    hipLaunchKernelGGL((gemm_s3_kernel<AL, BL, 3>), grid, dim3(S3_NT), 0, c->cur, g);
   else if (va && vb)
     gemm_dispatch<AL, BL, 4, 4>(p, grid, c->cur, g);
   else if (va)

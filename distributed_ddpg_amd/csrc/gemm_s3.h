@@ -21,11 +21,16 @@
 
 namespace ddpg {
 
-constexpr int S3_PLANE = 128 * H_ROW;                  // bf16 per plane (one operand, one stage)
-constexpr int S3_STAGE = 3 * S3_PLANE;                 // one operand, one stage
-constexpr int S3_SMEM_HALFS = 2 * 2 * S3_STAGE;        // 2 operands x 2 stages
-constexpr int S3_SMEM = (S3_SMEM_HALFS / 2 > TileCfg<128, 128>::EPI) ? S3_SMEM_HALFS / 2
-                                                                     : TileCfg<128, 128>::EPI;
+constexpr int S3_PLANE = 128 * H_ROW;  // bf16 per plane (one operand, one stage)
+// NP = 3: fp32 via the three-plane split; NP = 1: plain bf16 operands (the
+// bf16 configuration), same kernel with one plane and one product.
+template <int NP>
+struct S3Cfg {
+  static constexpr int STAGE = NP * S3_PLANE;      // one operand, one stage (bf16)
+  static constexpr int HALFS = 2 * 2 * STAGE;      // 2 operands x 2 stages
+  static constexpr int SMEM = (HALFS / 2 > TileCfg<128, 128>::EPI) ? HALFS / 2
+                                                                   : TileCfg<128, 128>::EPI;
+};
 
 constexpr int S3_NT = 512;  // 8 waves: 2 along M x 4 along N, wave tile 64 x 32
 
@@ -57,7 +62,7 @@ DDPG_DEV void split3_pair(f32x2v x, bf16x2& h, bf16x2& m, bf16x2& l) {
 // Per-thread pointers are set once and advanced one k-tile per load; rows out
 // of range read a clamped address and are zeroed (no branches), and only a
 // partial last k-tile checks k.
-template <int L>
+template <int L, int NP>
 struct StageS3 {
   float v[8];
   const float* p[2];
@@ -110,34 +115,45 @@ struct StageS3 {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int f = i * S3_NT + tid, r = f >> 3, kq = f & 7;
-        bf16x2 h0, m0, l0, h1, m1, l1;
-        split3_pair(f32x2v{v[4 * i], v[4 * i + 1]}, h0, m0, l0);
-        split3_pair(f32x2v{v[4 * i + 2], v[4 * i + 3]}, h1, m1, l1);
         __bf16* q = lds + r * H_ROW + 4 * kq;
-        *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
-        *reinterpret_cast<bf16x4*>(q + S3_PLANE) = bf16x4{m0[0], m0[1], m1[0], m1[1]};
-        *reinterpret_cast<bf16x4*>(q + 2 * S3_PLANE) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+        if constexpr (NP == 1) {
+          const bf16x2 h0 = __builtin_convertvector(f32x2v{v[4 * i], v[4 * i + 1]}, bf16x2);
+          const bf16x2 h1 = __builtin_convertvector(f32x2v{v[4 * i + 2], v[4 * i + 3]}, bf16x2);
+          *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+        } else {
+          bf16x2 h0, m0, l0, h1, m1, l1;
+          split3_pair(f32x2v{v[4 * i], v[4 * i + 1]}, h0, m0, l0);
+          split3_pair(f32x2v{v[4 * i + 2], v[4 * i + 3]}, h1, m1, l1);
+          *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+          *reinterpret_cast<bf16x4*>(q + S3_PLANE) = bf16x4{m0[0], m0[1], m1[0], m1[1]};
+          *reinterpret_cast<bf16x4*>(q + 2 * S3_PLANE) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+        }
       }
     } else {
       const int kp = tid & 15, rq = tid >> 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // row 4rq+i gets k = 2kp, 2kp+1
-        bf16x2 hh, mm, ll;
-        split3_pair(f32x2v{v[i], v[4 + i]}, hh, mm, ll);
         __bf16* q = lds + (4 * rq + i) * H_ROW + 2 * kp;
-        *reinterpret_cast<bf16x2*>(q) = hh;
-        *reinterpret_cast<bf16x2*>(q + S3_PLANE) = mm;
-        *reinterpret_cast<bf16x2*>(q + 2 * S3_PLANE) = ll;
+        if constexpr (NP == 1) {
+          *reinterpret_cast<bf16x2*>(q) = __builtin_convertvector(f32x2v{v[i], v[4 + i]}, bf16x2);
+        } else {
+          bf16x2 hh, mm, ll;
+          split3_pair(f32x2v{v[i], v[4 + i]}, hh, mm, ll);
+          *reinterpret_cast<bf16x2*>(q) = hh;
+          *reinterpret_cast<bf16x2*>(q + S3_PLANE) = mm;
+          *reinterpret_cast<bf16x2*>(q + 2 * S3_PLANE) = ll;
+        }
       }
     }
   }
 };
 
-template <int AL, int BL>
+template <int AL, int BL, int NP>
 __global__ __launch_bounds__(S3_NT, 1) void gemm_s3_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float smem[S3_SMEM];
+  using C = S3Cfg<NP>;
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
   __bf16* const As0 = reinterpret_cast<__bf16*>(smem);   // [stage][plane][128][H_ROW]
-  __bf16* const Bs0 = As0 + 2 * S3_STAGE;
+  __bf16* const Bs0 = As0 + 2 * C::STAGE;
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -166,9 +182,9 @@ __global__ __launch_bounds__(S3_NT, 1) void gemm_s3_kernel(GemmArgs g) {
     const __bf16* b_s = Bs + (wn * 32 + li) * H_ROW + 8 * h;
 #pragma unroll
     for (int ks = 0; ks < GBK / 16; ++ks) {
-      bf16x8 av[3][2], bv[3];  // [plane][tile]
+      bf16x8 av[NP][2], bv[NP];  // [plane][tile]
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
           av[p][i] =
@@ -177,28 +193,30 @@ __global__ __launch_bounds__(S3_NT, 1) void gemm_s3_kernel(GemmArgs g) {
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        // small terms first: lh, mm, hl, mh, hm, hh  (planes 0 = h, 1 = m, 2 = l)
         f32x16 c = acc[i][0];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
+        if constexpr (NP == 3) {
+          // small terms first: lh, mm, hl, mh, hm, hh  (planes 0 = h, 1 = m, 2 = l)
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
+        }
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], c, 0, 0, 0);
         acc[i][0] = c;
       }
     }
   };
   if (nk > 0) {
-    StageS3<AL> sa0, sa1;
-    StageS3<BL> sb0, sb1;
+    StageS3<AL, NP> sa0, sa1;
+    StageS3<BL, NP> sb0, sb1;
     sa0.init(g.A, g.lda, g.M, m0, kbeg, tid);
     sb0.init(g.B, g.ldb, g.N, n0, kbeg, tid);
     sa1 = sa0;
     sb1 = sb0;
     const int klen = kend - kbeg;
-    __bf16* const A1 = As0 + S3_STAGE;
-    __bf16* const B1 = Bs0 + S3_STAGE;
+    __bf16* const A1 = As0 + C::STAGE;
+    __bf16* const B1 = Bs0 + C::STAGE;
     sa0.load(0, klen);
     sb0.load(0, klen);
     sa1.load(1, klen - GBK);
