@@ -1,0 +1,109 @@
+// Microbenchmark (tuning aid, not product code): thin_k_kernel durations at
+// the C3 shapes (M = 4096, N = 1024, K = 64 / 16) with parts of its epilogue
+// switched off, to see where the time goes.  Prints avg us per launch.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+__device__ unsigned long long g_st[8192 * 5];
+#define TK_STAMP(i)                                                                        \
+  if (threadIdx.x == 0)                                                                    \
+    g_st[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 5 + (i)] =      \
+        __builtin_amdgcn_s_memtime();
+#include "../distributed_ddpg_amd/csrc/thin_k.h"
+#include <vector>
+#include <algorithm>
+
+// per-phase block averages and whole-grid span of the LAST launch (core clocks)
+static void phases(const char* tag, int nblocks) {
+  std::vector<unsigned long long> h(nblocks * 5);
+  hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_st), h.size() * 8);
+  unsigned long long t0 = ~0ull, t3 = 0;
+  double d[3] = {0, 0, 0};
+  for (int b = 0; b < nblocks; ++b) {
+    const unsigned long long* s = &h[b * 5];
+    t0 = std::min(t0, s[0]);
+    t3 = std::max(t3, s[3]);
+    for (int i = 0; i < 3; ++i) d[i] += double(s[i + 1] - s[i]) / nblocks;
+  }
+  // start-time spread: how late the last block starts
+  unsigned long long smax = 0;
+  for (int b = 0; b < nblocks; ++b) smax = std::max(smax, h[b * 5] - t0);
+  printf("   %s: span %llu clk, last start +%llu, per block: stage %.0f mfma %.0f epi %.0f\n", tag,
+         t3 - t0, smax, d[0], d[1], d[2]);
+}
+
+using namespace ddpg;
+
+static float time_it(const TkArgs& a, int nparts, int reps) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  int nmax = std::max(a.p[0].N, nparts > 1 ? a.p[1].N : 0);
+  dim3 grid((nmax + TK_COLS - 1) / TK_COLS, (a.M + TK_ROWS - 1) / TK_ROWS, nparts);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(thin_k_kernel, grid, dim3(TK_NT), 0, 0, a);
+  hipEventRecord(e0);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(thin_k_kernel, grid, dim3(TK_NT), 0, 0, a);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  return 1e3f * ms / reps;
+}
+
+int main() {
+  const int M = 4096, N = 1024;
+  float *X, *W, *bias, *out, *aux, *cs;
+  hipMalloc(&X, (size_t)M * 64 * 4);
+  hipMalloc(&W, (size_t)64 * N * 4);
+  hipMalloc(&bias, N * 4);
+  hipMalloc(&out, (size_t)M * 2 * N * 4);
+  hipMalloc(&aux, (size_t)M * N * 4);
+  hipMalloc(&cs, (size_t)64 * N * 4);
+  hipMemset(X, 0, (size_t)M * 64 * 4);
+  hipMemset(W, 0, (size_t)64 * N * 4);
+  hipMemset(bias, 0, N * 4);
+  hipMemset(aux, 0, (size_t)M * N * 4);
+  TkPart p;
+  memset(&p, 0, sizeof p);
+  p.X = X; p.ldx = 64; p.K = 64; p.W = W; p.ldw = N; p.N = N; p.bias = bias; p.act = 1;
+  p.out = out; p.ldo = 2 * N;
+  TkArgs a;
+  memset(&a, 0, sizeof a);
+  a.M = M;
+  a.p[0] = p;
+  printf("K64 bias+elu+store           %.2f us\n", time_it(a, 1, 200));
+  phases("K64", 8 * 64);
+  a.p[0].act = 0;
+  printf("K64 bias+store (no elu)      %.2f us\n", time_it(a, 1, 200));
+  a.p[0].out = nullptr;
+  printf("K64 no store                 %.2f us\n", time_it(a, 1, 200));
+  phases("K64 nostore", 8 * 64);
+  a.p[0] = p;
+  a.p[0].K = 8;
+  a.p[0].ldx = 8;
+  printf("K8 bias+elu+store            %.2f us\n", time_it(a, 1, 200));
+  phases("K8", 8 * 64);
+  a.p[0] = p;
+  a.p[1] = p;
+  a.p[1].out = out + N;
+  a.p[1].K = 16; a.p[1].ldx = 16;
+  printf("2 parts K64|K16              %.2f us\n", time_it(a, 2, 200));
+  // dz2: K = 16, w_nk, aux, colsum, no bias / act
+  TkPart q = p;
+  q.K = 16; q.ldx = 16; q.w_nk = 1; q.ldw = 16; q.bias = nullptr; q.act = 0;
+  q.aux = aux; q.ldaux = N; q.ldo = N; q.colsum = cs; q.ld_colsum = N;
+  a.p[0] = q;
+  printf("dz2 K16 w_nk aux colsum      %.2f us\n", time_it(a, 1, 200));
+  // pure write of 16 MB for reference
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  for (int i = 0; i < 50; ++i) hipMemsetAsync(out, 0, (size_t)M * N * 4);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("hipMemset 16 MB              %.2f us\n", 1e3f * ms / 50);
+  return 0;
+}
