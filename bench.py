@@ -287,6 +287,10 @@ def main():
                         "per_step": v["launches"] / args.profile_steps,
                         "ms_per_step": round(v["ms"] / args.profile_steps, 4)}
                     for k, v in sorted(by_kernel.items(), key=lambda kv: -kv[1]["ms"])},
+        # the same launches split by call site ("<kernel>|<phase>")
+        "kernels_by_phase": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
+                                 "per_step": v["launches"] / args.profile_steps}
+                             for k, v in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])},
     }
     hbm = {}
     for key in ("adam", "soft_update", "gather"):

@@ -17,6 +17,7 @@
 #include "gemm_f32.h"
 #include "gemm_bf16.h"
 #include "gemm_s3.h"
+#include "thin_k.h"
 #include "kernels.h"
 #include "sampler.h"
 #include "small_batch.h"
@@ -358,6 +359,14 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   const bool s3 = !bf && use_s3(c, M, N, vec);
   GemmPlan p = make_plan(M, N, K, splits, cap, bf || s3);
   if (M <= 0 || N <= 0) return p;
+  {  // the element-wise combinations gemm_epilogue is specialised on
+    const bool b = e.bias != nullptr;
+    const bool ok = (!b && e.act == 0 && e.post == 0) || (b && e.act == 1 && e.post == 0) ||
+                    (b && e.act == 1 && e.post == 2) || (!b && e.act == 0 && e.post == 1) ||
+                    (b && e.act == 0 && e.post == 0);
+    if (!ok) throw einval("gemm %s: unsupported epilogue (bias %d act %d post %d)", name, b, e.act,
+                          e.post);
+  }
   GemmArgs g;
   g.A = A;
   g.B = B;
@@ -417,6 +426,68 @@ static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec) {
   return g_gemm_s3 && c->cfg.dtype == DDPG_FP32 && vec && M >= 128 && N >= 128;
 }
 
+// Thin-K layers (thin_k.h) of fp32 contexts: K <= 64 and multiple of 8,
+// 4-aligned widths / leading dims, 16-byte aligned operands (anything else goes
+// through the GEMMs).  env DDPG_THINK=0 routes every such layer to the GEMMs.
+static int g_thin_k = -1;
+static bool tk_valid(const TkPart& q) {
+  return q.K >= TK_KALIGN && q.K % TK_KALIGN == 0 && q.K <= TK_MAXK && q.ldx % 4 == 0 && q.ldw % 4 == 0 &&
+         q.N % 4 == 0 && q.ldo % 4 == 0 && aligned16(q.X) && aligned16(q.W) &&
+         (!q.out || aligned16(q.out)) && (!q.bias || aligned16(q.bias)) &&
+         (!q.aux || (q.ldaux % 4 == 0 && aligned16(q.aux)));
+}
+
+static TkPart tk_part(const float* X, int ldx, int K, const float* W, int ldw, int w_nk, int N,
+                      const float* bias, int act, float* out, int ldo) {
+  TkPart p;
+  memset(&p, 0, sizeof p);
+  p.X = X;
+  p.ldx = ldx;
+  p.K = K;
+  p.W = W;
+  p.ldw = ldw;
+  p.w_nk = w_nk;
+  p.N = N;
+  p.bias = bias;
+  p.act = act;
+  p.out = out;
+  p.ldo = ldo;
+  return p;
+}
+
+// Launch 1 or 2 thin-K parts over M rows; returns the number of 64-row blocks
+// (the row count of colsum partials), or 0 (nothing launched) when the layer
+// is not eligible and the caller must use the GEMM.
+static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M) {
+  if (g_thin_k < 0) {
+    const char* v = getenv("DDPG_THINK");
+    g_thin_k = !(v && atoi(v) == 0);
+  }
+  if (!g_thin_k || c->cfg.dtype != DDPG_FP32) return 0;
+  for (int i = 0; i < nparts; ++i)
+    if (!tk_valid(parts[i])) return 0;
+  TkArgs a;
+  memset(&a, 0, sizeof a);
+  int nmax = 0;
+  double flops = 0, bytes = 0;
+  for (int i = 0; i < nparts; ++i) {
+    a.p[i] = parts[i];
+    nmax = std::max(nmax, parts[i].N);
+    flops += 2.0 * M * parts[i].N * (double)parts[i].K;
+    bytes += 4.0 * ((double)M * parts[i].K + (double)parts[i].K * parts[i].N +
+                    (double)M * parts[i].N);
+  }
+  a.M = M;
+  const int mt = ceil_div(M, TK_ROWS);
+  char key[96];
+  snprintf(key, sizeof key, "thin_k_kernel|%s", name);
+  ProfScope ps(c, key, flops, bytes);
+  hipLaunchKernelGGL(thin_k_kernel, dim3(ceil_div(nmax, TK_COLS), mt, nparts), dim3(TK_NT), 0,
+                     c->cur, a);
+  HIP_TRY(hipGetLastError());
+  return mt;
+}
+
 // ====================================================================== building blocks
 static const float* P(ddpg_ctx* c, const float* base, const Tensor& t) { return base + t.off; }
 
@@ -426,11 +497,16 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
                       float* h2, float* o, float* mu) {
   const Layout& L = c->L;
   GemmEpi e = epi_none();
-  e.out = h1;
-  e.ldo = c->ldAH1;
-  e.bias = P(c, base, L.a[AB1]);
-  e.act = 1;
-  gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.a[AW1]), c->AH1, B, c->AH1, c->S, e);
+  const TkPart tp = tk_part(s, c->ldS, c->S, P(c, base, L.a[AW1]), c->AH1, 0, c->AH1,
+                            P(c, base, L.a[AB1]), 1, h1, c->ldAH1);
+  if (!thin_k_launch(c, "fwd", &tp, 1, B)) {
+    e.out = h1;
+    e.ldo = c->ldAH1;
+    e.bias = P(c, base, L.a[AB1]);
+    e.act = 1;
+    gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.a[AW1]), c->AH1, B, c->AH1, c->S,
+                            e);
+  }
   e = epi_none();
   e.out = h2;
   e.ldo = c->ldAH2;
@@ -458,14 +534,23 @@ static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const floa
                       float* cat, float* h_out, int mode, float* dhp_out) {
   const Layout& L = c->L;
   GemmEpi e = epi_none();
-  e.out = cat;
-  e.ldo = c->ldC;
-  e.bias = P(c, base, L.c[CBS]);
-  e.act = 1;
-  gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1, c->S, e);
-  e.out = cat + c->CH1;
-  e.bias = P(c, base, L.c[CBA]);
-  gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1, c->A, e);
+  // [state branch | action branch] of the concat in one launch
+  const TkPart tp[2] = {tk_part(s, c->ldS, c->S, P(c, base, L.c[CWS]), c->CH1, 0, c->CH1,
+                                P(c, base, L.c[CBS]), 1, cat, c->ldC),
+                        tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1,
+                                P(c, base, L.c[CBA]), 1, cat + c->CH1, c->ldC)};
+  if (!thin_k_launch(c, "fwd", tp, 2, B)) {
+    e.out = cat;
+    e.ldo = c->ldC;
+    e.bias = P(c, base, L.c[CBS]);
+    e.act = 1;
+    gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1, c->S,
+                            e);
+    e.out = cat + c->CH1;
+    e.bias = P(c, base, L.c[CBA]);
+    gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1, c->A,
+                            e);
+  }
   e = epi_none();
   e.bias = P(c, base, L.c[CBH]);
   e.act = 1;
@@ -679,17 +764,26 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
                                          B, e, 0, c->split_cap_W3);
   c->cur = main;
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
-  e = epi_none();
-  e.post = 1;
-  e.aux = c->h2;
-  e.ldaux = c->ldAH2;
-  e.out = c->dz2;
-  e.ldo = c->ldAH2;
-  e.colsum = c->colpart;
-  e.ld_colsum = c->AH2;
-  GemmPlan pz2 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]), c->A,
-                                         B, c->AH2, c->A, e);
-  const int mt2 = pz2.mt(B);
+  TkPart tp = tk_part(c->dz3, c->ldA, c->A, P(c, c->theta, L.a[AW3]), c->A, 1, c->AH2, nullptr,
+                      0, c->dz2, c->ldAH2);
+  tp.aux = c->h2;
+  tp.ldaux = c->ldAH2;
+  tp.colsum = c->colpart;
+  tp.ld_colsum = c->AH2;
+  int mt2 = thin_k_launch(c, "dx", &tp, 1, B);
+  if (!mt2) {
+    e = epi_none();
+    e.post = 1;
+    e.aux = c->h2;
+    e.ldaux = c->ldAH2;
+    e.out = c->dz2;
+    e.ldo = c->ldAH2;
+    e.colsum = c->colpart;
+    e.ld_colsum = c->AH2;
+    GemmPlan pz2 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz3, c->ldA, P(c, c->theta, L.a[AW3]),
+                                           c->A, B, c->AH2, c->A, e);
+    mt2 = pz2.mt(B);
+  }
   // dW2 = h1^T . dz2   (aux[0] waits for dz2, then runs beside dz1)
   if (par) {
     fork_to(c, 7, main, c->aux[0]);

@@ -72,12 +72,6 @@ struct GemmArgs {
   GemmEpi e;
 };
 
-
-// ---------------------------------------------------------------- epilogue
-// Accumulator layout (32x32 MFMA, dtype independent on gfx950): lane l holds
-// column l&31 of tile (i, j); register r holds row (r&3) + 8(r>>2) + 4(l>>5).
-// smem must hold TileCfg<BM,BN>::EPI floats and be free (all staging reads
-// done) on entry.
 // XCD-aware tile order (guide T1, bijective form): hardware deals workgroups
 // round-robin over the 8 XCDs, so consecutive linear ids land on different
 // L2s.  Remap so each XCD owns a contiguous run of row-major tiles (whole
@@ -100,6 +94,70 @@ DDPG_DEV void xcd_tile(int& bx, int& by, int on) {
 
 // WGN: waves along N (2 for the 4-wave kernels, 4 for the 8-wave gemm_s3);
 // the block always has 2 waves along M, each owning BM/2 rows.
+// The __syncthreads() that gemm_epilogue executes for these epilogue flags:
+// waves of a block that hold no accumulators (gemm_s3's staging waves) call
+// this instead so that every wave passes the same barriers.  Keep in step
+// with the barriers in gemm_epilogue below.
+DDPG_DEV void gemm_epilogue_barriers(const GemmEpi& e) {
+  if (!e.out && !e.colsum && !e.proj_out) return;
+  for (int pass = 0; pass < 2; ++pass) {
+    __syncthreads();
+    __syncthreads();
+  }
+  if (e.colsum) __syncthreads();
+}
+
+// Element-wise part of the epilogue on one wave's accumulators, specialised
+// on the flag combinations the learner uses (BIAS: + bias[n]; ACT 1: elu;
+// POST 1: * EluGrad factor of aux[m][n]; POST 2: pw[n] * EluGrad factor of v).
+// Values outside the M x N range become 0 (they feed the row reductions).
+template <int BM, int BN, int WGN, bool BIAS, int ACT, int POST>
+DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& e, int M, int N,
+                        int n0, int m0, int wm, int wn, int h, int li) {
+  constexpr int TM = BM / 64, TN = BN / (32 * WGN);
+  constexpr int WR = BM / 2, WC = BN / WGN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WC + j * 32 + li;
+      const bool nok = n < N;
+      const float bn = (BIAS && nok) ? e.bias[n] : 0.f;
+      const float pwn = (POST == 2 && nok) ? e.pw[n] : 0.f;
+      float av[16];
+      if constexpr (POST == 1) {  // all 16 loads in flight before the first use
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float* q = (nok && m < M) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
+          av[r] = *q;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v = acc[i][j][r];
+        if constexpr (BIAS) v = __fadd_rn(v, bn);
+        if constexpr (ACT == 1) v = elu_f(v);
+        if constexpr (POST == 1) v = __fmul_rn(v, elu_grad_factor(av[r]));
+        if constexpr (POST == 2) v = __fmul_rn(pwn, elu_grad_factor(v));
+        acc[i][j][r] = (nok && m < M) ? v : 0.f;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- epilogue
+// Accumulator layout (32x32 MFMA, dtype independent on gfx950): lane l holds
+// column l&31 of tile (i, j); register r holds row (r&3) + 8(r>>2) + 4(l>>5).
+// smem must hold TileCfg<BM,BN>::EPI floats and be free (all staging reads
+// done) on entry.  WGN: waves along N; the accumulator waves are 2 x WGN
+// (threads 0 .. 2*WGN*64-1), each owning BM/2 rows.
+//
+// The element-wise ops run in registers; the tile then goes through LDS one
+// wave row (BM/2 rows) at a time, from where it is stored as float4 rows
+// (1 KiB per wave instruction instead of 128-B column pieces) and reduced
+// (bias-gradient column sums, thin projections).
 template <int BM, int BN, int WGN = 2>
 DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem,
                             const GemmArgs& g,
@@ -114,35 +172,23 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   const GemmEpi& e = g.e;
   const int M = g.M, N = g.N;
   float* outp = e.out ? e.out + (size_t)z * e.out_split_stride : nullptr;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WC + j * 32 + li;
-      const bool nok = n < N;
-      const float bn = (nok && e.bias) ? e.bias[n] : 0.f;
-      const float pwn = (nok && e.post == 2) ? e.pw[n] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float v = acc[i][j][r];
-        if (nok && m < M) {
-          if (e.bias) v = __fadd_rn(v, bn);
-          if (e.act == 1) v = elu_f(v);
-          if (e.post == 1) v = __fmul_rn(v, elu_grad_factor(e.aux[(size_t)m * e.ldaux + n]));
-          else if (e.post == 2) v = __fmul_rn(pwn, elu_grad_factor(v));
-          if (outp) outp[(size_t)m * e.ldo + n] = v;
-        } else {
-          v = 0.f;
-        }
-        acc[i][j][r] = v;
-      }
-    }
-  }
 
-  if (!e.colsum && !e.proj_out) return;
+  const bool bias = e.bias != nullptr;
+  if (!bias && e.act == 0 && e.post == 0)
+    epi_apply<BM, BN, WGN, false, 0, 0>(acc, e, M, N, n0, m0, wm, wn, h, li);
+  else if (bias && e.act == 1 && e.post == 0)
+    epi_apply<BM, BN, WGN, true, 1, 0>(acc, e, M, N, n0, m0, wm, wn, h, li);
+  else if (bias && e.act == 1 && e.post == 2)
+    epi_apply<BM, BN, WGN, true, 1, 2>(acc, e, M, N, n0, m0, wm, wn, h, li);
+  else if (!bias && e.act == 0 && e.post == 1)
+    epi_apply<BM, BN, WGN, false, 0, 1>(acc, e, M, N, n0, m0, wm, wn, h, li);
+  else if (bias && e.act == 0 && e.post == 0)
+    epi_apply<BM, BN, WGN, true, 0, 0>(acc, e, M, N, n0, m0, wm, wn, h, li);
+  else  // not used by the learner; the host rejects other combinations
+    __builtin_trap();
 
-  // Row-wise reductions through LDS, WR tile rows (one wave row) per pass.
+  if (!outp && !e.colsum && !e.proj_out) return;
+
   constexpr int VS_LD = TC::VS_LD;
   float* Vs = smem;                      // [WR][VS_LD]
   float* Wps = smem + WR * VS_LD;        // [BN][PN]
@@ -155,6 +201,10 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
                                           : 0.f;
     }
   }
+  // float4 row stores need 4-aligned widths / leading dims and a 16-B base
+  const bool vst = outp && ((N | e.ldo) & 3) == 0 && (e.out_split_stride & 3) == 0 &&
+                   ((uintptr_t)outp & 15) == 0;
+  constexpr int C4 = BN / 4, RPR = NT / C4;  // float4 columns per row, rows per round
   constexpr int CG = NT / BN;  // column-sum row groups
   float csum = 0.f;
 #pragma unroll
@@ -171,6 +221,25 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           }
     }
     __syncthreads();
+    if (outp) {
+      const int c4 = tid % C4, rr0 = tid / C4, n = n0 + 4 * c4;
+#pragma unroll 4
+      for (int rr = rr0; rr < WR; rr += RPR) {
+        const int m = m0 + pass * WR + rr;
+        if (m < M) {
+          const float4 v = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 4 * c4);
+          float* o = outp + (size_t)m * e.ldo + n;
+          if (vst) {
+            if (n < N) *reinterpret_cast<float4*>(o) = v;
+          } else {
+            if (n < N) o[0] = v.x;
+            if (n + 1 < N) o[1] = v.y;
+            if (n + 2 < N) o[2] = v.z;
+            if (n + 3 < N) o[3] = v.w;
+          }
+        }
+      }
+    }
     if (e.colsum) {
       const int col = tid % BN, grp = tid / BN;
 #pragma unroll 4
