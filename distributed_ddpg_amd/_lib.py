@@ -20,6 +20,9 @@ DDPG_EINVAL, DDPG_EHIP, DDPG_ENOMEM, DDPG_ESTATE, DDPG_ECOMM = -1, -2, -3, -4, -
 FP32, BF16 = 0, 1
 ACTOR, ACTOR_TARGET, CRITIC, CRITIC_TARGET = 0, 1, 2, 3
 ACTOR_ADAM_M, ACTOR_ADAM_V, CRITIC_ADAM_M, CRITIC_ADAM_V = 4, 5, 6, 7
+ACTOR_GRAD, CRITIC_GRAD = 8, 9
+REPLAY_F64 = 1
+ABI_VERSION = 2
 SOFT_ACTOR, SOFT_CRITIC = 1, 2
 
 
@@ -88,13 +91,18 @@ PROTOTYPES = [
     ("ddpg_sampler_getrandbits32", _c.c_int, [_P, _u32p, _c.c_int]),
     ("ddpg_replay_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int64, _c.c_int64,
                                       _c.POINTER(_P)]),
+    ("ddpg_replay_create_ex", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int64, _c.c_int64,
+                                         _c.c_int, _c.POINTER(_P)]),
+    ("ddpg_replay_is_f64", _c.c_int, [_P]),
     ("ddpg_replay_destroy", None, [_P]),
     ("ddpg_replay_last_error", _c.c_char_p, [_P]),
     ("ddpg_replay_add", _c.c_int, [_P, _fp, _fp, _fp, _u8p, _fp, _c.c_int]),
+    ("ddpg_replay_add_f64", _c.c_int, [_P, _dp, _fp, _dp, _u8p, _dp, _c.c_int]),
     ("ddpg_replay_size", _c.c_int64, [_P]),
     ("ddpg_replay_total_added", _c.c_int64, [_P]),
     ("ddpg_replay_clear", _c.c_int, [_P]),
     ("ddpg_replay_sample_batch", _c.c_int, [_P, _c.c_int, _fp, _fp, _fp, _u8p, _fp, _i64p]),
+    ("ddpg_replay_sample_batch_f64", _c.c_int, [_P, _c.c_int, _dp, _fp, _dp, _u8p, _dp, _i64p]),
     ("ddpg_learner_step", _c.c_int, [_P, _P, _c.c_int, _c.POINTER(Stats)]),
     ("ddpg_learner_step_indices", _c.c_int, [_P, _P, _i64p, _c.c_int, _c.POINTER(Stats)]),
     ("ddpg_read_stats", _c.c_int, [_P, _dp, _dp, _i64p, _c.c_int]),
@@ -110,7 +118,7 @@ for _name, _res, _args in PROTOTYPES:
     _f.restype = _res
     _f.argtypes = _args
 
-if lib.ddpg_abi_version() != 1:
+if lib.ddpg_abi_version() != ABI_VERSION:
     raise ImportError("libddpg_hip.so ABI version mismatch")
 
 
@@ -123,6 +131,10 @@ def check(rc, ctx=None):
 
 def fptr(a):
     return a.ctypes.data_as(_fp)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp)
 
 
 def f32(x, shape=None):

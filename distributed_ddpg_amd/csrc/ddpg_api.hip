@@ -108,25 +108,36 @@ struct ProfAgg {
 // ====================================================================== replay
 struct ddpg_replay {
   int device = 0, S = 0, A = 0;
+  // f64: s, s2 and r are kept as float64, the values the reference's deque
+  // holds (replay_buffer.py:22-26), so sample_batch returns them exactly and
+  // the scaler sees the unrounded state; a / t are fp32 / 0-1 either way.
+  bool f64 = false;
   int64_t cap = 0, count = 0, total = 0;
-  float *rs = nullptr, *ra = nullptr, *rr = nullptr, *rt = nullptr, *rs2 = nullptr;
+  float *ra = nullptr, *rt = nullptr;
+  float *rs = nullptr, *rr = nullptr, *rs2 = nullptr;      // fp32 ring
+  double *rsd = nullptr, *rrd = nullptr, *rs2d = nullptr;  // float64 ring
   Sampler sampler;
   hipStream_t stream = nullptr;
   std::string err;
-  // host staging for single-row adds
-  std::vector<float> st_s, st_a, st_r, st_t, st_s2;
+  // host staging for single-row adds (s, s2, r in the ring's precision)
+  std::vector<unsigned char> st_s, st_s2, st_r;
+  std::vector<float> st_a, st_t;
   int64_t st_first = 0;  // insertion index of first staged row
   int st_n = 0;
   std::vector<int64_t> tmp_idx;
   std::vector<int> tmp_slot;
   int* d_slots = nullptr;
   int d_slots_cap = 0;
-  float* d_tmp = nullptr;
+  unsigned char* d_tmp = nullptr;
   size_t d_tmp_cap = 0;
   // recorded by learner contexts after their gather; ring writes wait on it so
   // a queued gather never reads rows that a later add overwrote
   hipEvent_t last_read = nullptr;
   explicit ddpg_replay(int64_t seed) : sampler(seed) {}
+  size_t es() const { return f64 ? 8 : 4; }  // bytes per s / s2 / r element
+  unsigned char* ps() const { return f64 ? (unsigned char*)rsd : (unsigned char*)rs; }
+  unsigned char* ps2() const { return f64 ? (unsigned char*)rs2d : (unsigned char*)rs2; }
+  unsigned char* pr() const { return f64 ? (unsigned char*)rrd : (unsigned char*)rr; }
 };
 
 static void replay_flush(ddpg_replay* rb);
@@ -154,6 +165,7 @@ struct ddpg_ctx {
   float* dpw = nullptr;          // [actor b1p, b2p, critic b1p, b2p]
   unsigned* dcounter = nullptr;  // [2]
   float* dstats = nullptr;       // [q_max, loss]
+  float* dstats_all = nullptr;   // [world][2] all-gathered stats (world > 1)
   double* dacc = nullptr;        // [qmax_sum, loss_sum, steps]
   double *dmean = nullptr, *dscale = nullptr;
   bool has_scaler = false;
@@ -630,6 +642,21 @@ static void allreduce(ddpg_ctx* c, float* buf, size_t n) {
   if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
 }
 
+// the logged stats of a data-parallel step are the
+// global-batch ones (ddpg.py:102-103) -- max over ranks of max(Q) and the sum
+// of the ranks' loss shares (each already scaled by 1/B_global).  One
+// all-gather of every rank's {q_max, loss}, then an ordered reduction that
+// every rank computes identically; it also feeds the running sums.
+static void stats_allreduce(ddpg_ctx* c) {
+  if (c->world <= 1 || !c->comm) return;
+  ProfScope ps(c, "rccl_stats", 0, 8.0 * c->world);
+  ncclResult_t r = ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cur);
+  if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cur, c->dstats_all, c->world,
+                     c->dstats, c->dacc);
+  HIP_TRY(hipGetLastError());
+}
+
 // TF ApplyAdam over one network's flat region.  advance: also advance its
 // beta powers right after (1:1 API path); the fused step advances both in
 // the soft-update kernel instead.
@@ -672,8 +699,10 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   if (nq < 0) nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
   {
     ProfScope ps(c, "critic_loss", 0, 0);
+    // world > 1: the per-step stats are reduced over ranks below, then accumulated
     hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->cur, c->qpart, nq, B,
-                       P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq, c->dstats, c->dacc);
+                       P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq, c->dstats,
+                       c->comm ? nullptr : c->dacc);
     HIP_TRY(hipGetLastError());
   }
   const int nchunk = ceil_div(B, kHeadRows);
@@ -741,6 +770,7 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.critic_begin, L.critic_end - L.critic_begin);
+  stats_allreduce(c);
   adam_launch(c, 1, !fused);
 }
 
@@ -946,10 +976,14 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
     a.rr = rb->rr;
     a.rt = rb->rt;
     a.rs2 = rb->rs2;
+    a.rsd = rb->rsd;
+    a.rs2d = rb->rs2d;
+    a.rrd = rb->rrd;
   }
   a.mean = c->has_scaler ? c->dmean : nullptr;
   a.sdev = c->has_scaler ? c->dscale : nullptr;
   a.theta = c->theta;
+  a.grad = c->grad;
   a.target = c->target;
   a.adam_m = c->adam_m;
   a.adam_v = c->adam_v;
@@ -1044,13 +1078,6 @@ static void check_b(ddpg_ctx* c, int B) {
   if (B <= 0 || B > c->Bmax) throw einval("batch %d outside [1, %d]", B, c->Bmax);
 }
 
-static void apply_scaler(ddpg_ctx* c, float* x, int B) {
-  if (!c->has_scaler) return;
-  hipLaunchKernelGGL(scale_rows_kernel, dim3(ceil_div(B * c->S, 256)), dim3(256), 0, c->stream, x,
-                     B, c->S, c->ldS, c->dmean, c->dscale);
-  HIP_TRY(hipGetLastError());
-}
-
 template <class F>
 static int guard(ddpg_ctx* c, F&& f) {
   try {
@@ -1088,7 +1115,7 @@ static void ctx_free(ddpg_ctx* c) {
                   (void*)c->sb_stamps})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
-                  (void*)c->dmean, (void*)c->dscale, (void*)c->dacc})
+                  (void*)c->dmean, (void*)c->dscale, (void*)c->dacc, (void*)c->dstats_all})
     if (p) (void)hipFree(p);
   for (auto st : c->aux)
     if (st) (void)hipStreamDestroy(st);
@@ -1401,7 +1428,8 @@ int ddpg_set_stream(ddpg_ctx* c, void* s) {
 // ---------------------------------------------------------------- parameters
 static void which_tensors(ddpg_ctx* c, int which, const Tensor** ts, int* nt, float** base) {
   const bool actor = which == DDPG_ACTOR || which == DDPG_ACTOR_TARGET ||
-                     which == DDPG_ACTOR_ADAM_M || which == DDPG_ACTOR_ADAM_V;
+                     which == DDPG_ACTOR_ADAM_M || which == DDPG_ACTOR_ADAM_V ||
+                     which == DDPG_ACTOR_GRAD;
   *ts = actor ? c->L.a : c->L.c;
   *nt = actor ? NA : NC;
   switch (which) {
@@ -1413,6 +1441,8 @@ static void which_tensors(ddpg_ctx* c, int which, const Tensor** ts, int* nt, fl
     case DDPG_CRITIC_ADAM_M: *base = c->adam_m; break;
     case DDPG_ACTOR_ADAM_V:
     case DDPG_CRITIC_ADAM_V: *base = c->adam_v; break;
+    case DDPG_ACTOR_GRAD:
+    case DDPG_CRITIC_GRAD: *base = c->grad; break;
     default: throw einval("bad parameter set %d", which);
   }
 }
@@ -1526,7 +1556,6 @@ int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_
       return;
     }
     upload_rows(c, c->s, c->ldS, s, B, c->S);
-    apply_scaler(c, c->s, B);
     actor_fwd(c, target ? c->target : c->theta, c->s, B, c->h1, nullptr, nullptr, c->mu);
     download_rows(c, a_out, c->mu, c->ldA, B, c->A);
   });
@@ -1537,7 +1566,6 @@ int ddpg_critic_forward(ddpg_ctx* c, int target, const float* s, const float* a,
   return guard(c, [&] {
     check_b(c, B);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
-    apply_scaler(c, c->s, B);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     const float* base = target ? c->target : c->theta;
     const int nq = critic_fwd(c, base, c->s, c->a, B, c->cat, nullptr, 1, nullptr);
@@ -1554,7 +1582,6 @@ int ddpg_critic_train(ddpg_ctx* c, const float* s, const float* a, const float* 
   return guard(c, [&] {
     check_b(c, B);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
-    apply_scaler(c, c->s, B);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     upload_rows(c, c->y, 1, y, B, 1);
     critic_train_dev(c, B, 1.0f / (float)(B * c->world), false);
@@ -1572,7 +1599,6 @@ int ddpg_critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int B, 
   return guard(c, [&] {
     check_b(c, B);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
-    apply_scaler(c, c->s, B);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     critic_action_grad(c, c->s, c->a, B, c->da, nullptr, nullptr);
     download_rows(c, da, c->da, c->ldA, B, c->A);
@@ -1583,7 +1609,6 @@ int ddpg_actor_train(ddpg_ctx* c, const float* s, const float* a_gradient, int B
   return guard(c, [&] {
     check_b(c, B);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
-    apply_scaler(c, c->s, B);
     // a_gradient as a single "partial" slab [1][B][A] for the dz3 finaliser
     HIP_TRY(hipMemcpyAsync(c->dain, a_gradient, (size_t)B * c->A * 4, hipMemcpyHostToDevice,
                            c->stream));
@@ -1632,29 +1657,42 @@ int ddpg_sampler_getrandbits32(ddpg_sampler* s, uint32_t* out, int n) {
 // ---------------------------------------------------------------- replay
 static constexpr int kStageRows = 1024;
 
-int ddpg_replay_create(int device, int S, int A, int64_t cap, int64_t seed, ddpg_replay** out) {
+static int replay_create_impl(int device, int S, int A, int64_t cap, int64_t seed, int flags,
+                              ddpg_replay** out) {
   if (!out) return DDPG_EINVAL;
   ddpg_replay* rb = new ddpg_replay(seed);
   int rc = rguard(rb, [&] {
     if (S <= 0 || A <= 0 || cap <= 0) throw einval("bad replay dims S=%d A=%d cap=%lld", S, A,
                                                    (long long)cap);
+    if (flags & ~DDPG_REPLAY_F64) throw einval("bad replay flags %d", flags);
     rb->device = device;
     rb->S = S;
     rb->A = A;
     rb->cap = cap;
+    rb->f64 = (flags & DDPG_REPLAY_F64) != 0;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&rb->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&rb->last_read, hipEventDisableTiming));
-    const size_t c = (size_t)cap;
-    HIP_TRY(hipMalloc(&rb->rs, c * S * 4));
-    HIP_TRY(hipMalloc(&rb->rs2, c * S * 4));
+    const size_t c = (size_t)cap, es = rb->es();
+    void *ps, *ps2, *pr;
+    HIP_TRY(hipMalloc(&ps, c * S * es));
+    HIP_TRY(hipMalloc(&ps2, c * S * es));
+    HIP_TRY(hipMalloc(&pr, c * es));
+    if (rb->f64) {
+      rb->rsd = (double*)ps;
+      rb->rs2d = (double*)ps2;
+      rb->rrd = (double*)pr;
+    } else {
+      rb->rs = (float*)ps;
+      rb->rs2 = (float*)ps2;
+      rb->rr = (float*)pr;
+    }
     HIP_TRY(hipMalloc(&rb->ra, c * A * 4));
-    HIP_TRY(hipMalloc(&rb->rr, c * 4));
     HIP_TRY(hipMalloc(&rb->rt, c * 4));
-    rb->st_s.resize((size_t)kStageRows * S);
-    rb->st_s2.resize((size_t)kStageRows * S);
+    rb->st_s.resize((size_t)kStageRows * S * es);
+    rb->st_s2.resize((size_t)kStageRows * S * es);
+    rb->st_r.resize((size_t)kStageRows * es);
     rb->st_a.resize((size_t)kStageRows * A);
-    rb->st_r.resize(kStageRows);
     rb->st_t.resize(kStageRows);
   });
   if (rc != DDPG_OK) {
@@ -1666,12 +1704,24 @@ int ddpg_replay_create(int device, int S, int A, int64_t cap, int64_t seed, ddpg
   return DDPG_OK;
 }
 
+int ddpg_replay_create(int device, int S, int A, int64_t cap, int64_t seed, ddpg_replay** out) {
+  return replay_create_impl(device, S, A, cap, seed, 0, out);
+}
+
+int ddpg_replay_create_ex(int device, int S, int A, int64_t cap, int64_t seed, int flags,
+                          ddpg_replay** out) {
+  return replay_create_impl(device, S, A, cap, seed, flags, out);
+}
+
+int ddpg_replay_is_f64(ddpg_replay* rb) { return rb && rb->f64 ? 1 : 0; }
+
 void ddpg_replay_destroy(ddpg_replay* rb) {
   if (!rb) return;
   (void)hipSetDevice(rb->device);
   if (rb->stream) (void)hipStreamSynchronize(rb->stream);
-  for (void* p : {(void*)rb->rs, (void*)rb->rs2, (void*)rb->ra, (void*)rb->rr, (void*)rb->rt,
-                  (void*)rb->d_slots, (void*)rb->d_tmp})
+  for (void* p : {(void*)rb->rs, (void*)rb->rs2, (void*)rb->rr, (void*)rb->rsd, (void*)rb->rs2d,
+                  (void*)rb->rrd, (void*)rb->ra, (void*)rb->rt, (void*)rb->d_slots,
+                  (void*)rb->d_tmp})
     if (p) (void)hipFree(p);
   if (rb->stream) (void)hipStreamDestroy(rb->stream);
   if (rb->last_read) (void)hipEventDestroy(rb->last_read);
@@ -1680,23 +1730,28 @@ void ddpg_replay_destroy(ddpg_replay* rb) {
 
 const char* ddpg_replay_last_error(ddpg_replay* rb) { return rb ? rb->err.c_str() : ""; }
 
-// copy n consecutive insertions starting at insertion index `first` into the ring
-static void ring_write(ddpg_replay* rb, int64_t first, int n, const float* s, const float* a,
-                       const float* r, const float* t, const float* s2) {
+// copy n consecutive insertions starting at insertion index `first` into the
+// ring; s, s2, r are already in the ring's precision (rb->es() bytes each)
+static void ring_write(ddpg_replay* rb, int64_t first, int n, const void* s, const float* a,
+                       const void* r, const float* t, const void* s2) {
+  const size_t es = rb->es(), S = rb->S, A = rb->A;
+  const unsigned char* bs = (const unsigned char*)s;
+  const unsigned char* bs2 = (const unsigned char*)s2;
+  const unsigned char* br = (const unsigned char*)r;
   int done = 0;
   while (done < n) {
     const int64_t slot = (first + done) % rb->cap;
-    const int run = (int)std::min<int64_t>(n - done, rb->cap - slot);
-    const size_t S = rb->S, A = rb->A;
-    HIP_TRY(hipMemcpyAsync(rb->rs + slot * S, s + done * S, run * S * 4, hipMemcpyHostToDevice,
-                           rb->stream));
-    HIP_TRY(hipMemcpyAsync(rb->rs2 + slot * S, s2 + done * S, run * S * 4,
+    const size_t run = (size_t)std::min<int64_t>(n - done, rb->cap - slot);
+    HIP_TRY(hipMemcpyAsync(rb->ps() + slot * S * es, bs + done * S * es, run * S * es,
                            hipMemcpyHostToDevice, rb->stream));
+    HIP_TRY(hipMemcpyAsync(rb->ps2() + slot * S * es, bs2 + done * S * es, run * S * es,
+                           hipMemcpyHostToDevice, rb->stream));
+    HIP_TRY(hipMemcpyAsync(rb->pr() + slot * es, br + done * es, run * es, hipMemcpyHostToDevice,
+                           rb->stream));
     HIP_TRY(hipMemcpyAsync(rb->ra + slot * A, a + done * A, run * A * 4, hipMemcpyHostToDevice,
                            rb->stream));
-    HIP_TRY(hipMemcpyAsync(rb->rr + slot, r + done, run * 4, hipMemcpyHostToDevice, rb->stream));
     HIP_TRY(hipMemcpyAsync(rb->rt + slot, t + done, run * 4, hipMemcpyHostToDevice, rb->stream));
-    done += run;
+    done += (int)run;
   }
 }
 
@@ -1709,44 +1764,82 @@ static void replay_flush(ddpg_replay* rb) {
   rb->st_n = 0;
 }
 
+extern "C++" {
+// n host values of type T into dst in the ring's precision (float or double)
+template <class T>
+static void to_ring(const ddpg_replay* rb, const T* src, size_t n, unsigned char* dst) {
+  if (rb->f64) {
+    double* d = (double*)dst;
+    for (size_t i = 0; i < n; ++i) d[i] = (double)src[i];
+  } else {
+    float* d = (float*)dst;
+    for (size_t i = 0; i < n; ++i) d[i] = (float)src[i];
+  }
+}
+
+// ReplayBuffer.add for n rows whose s, s2, r are float (T = float) or float64
+// (T = double); converted to the ring's precision on the host.
+template <class T>
+static void replay_add_impl(ddpg_replay* rb, const T* s, const float* a, const T* r,
+                            const uint8_t* t, const T* s2, int n) {
+  if (n < 0) throw einval("negative row count");
+  if (n > 0 && (!s || !a || !r || !t || !s2)) throw einval("null row array");
+  HIP_TRY(hipSetDevice(rb->device));
+  const size_t S = rb->S, A = rb->A, es = rb->es();
+  if (n >= kStageRows) {  // bulk insert
+    replay_flush(rb);
+    if (rb->last_read) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->last_read, 0));
+    // only the last `cap` rows can survive; skip the ones that would be overwritten
+    const int64_t skip = n > rb->cap ? n - rb->cap : 0;
+    const size_t m = (size_t)(n - skip);
+    std::vector<float> tf(m);
+    for (size_t i = 0; i < m; ++i) tf[i] = t[skip + i] ? 1.f : 0.f;
+    const bool same = (sizeof(T) == es);  // caller's arrays already in ring precision
+    std::vector<unsigned char> cs, cs2, cr;
+    const void *ps = s + skip * S, *ps2 = s2 + skip * S, *pr = r + skip;
+    if (!same) {
+      cs.resize(m * S * es);
+      cs2.resize(m * S * es);
+      cr.resize(m * es);
+      to_ring(rb, s + skip * S, m * S, cs.data());
+      to_ring(rb, s2 + skip * S, m * S, cs2.data());
+      to_ring(rb, r + skip, m, cr.data());
+      ps = cs.data();
+      ps2 = cs2.data();
+      pr = cr.data();
+    }
+    ring_write(rb, rb->total + skip, (int)m, ps, a + skip * A, pr, tf.data(), ps2);
+    HIP_TRY(hipStreamSynchronize(rb->stream));
+    rb->total += n;
+    rb->count = std::min<int64_t>(rb->total, rb->cap);
+    return;
+  }
+  int done = 0;
+  while (done < n) {
+    if (rb->st_n == 0) rb->st_first = rb->total;
+    const int take = std::min(n - done, kStageRows - rb->st_n);
+    to_ring(rb, s + done * S, take * S, rb->st_s.data() + rb->st_n * S * es);
+    to_ring(rb, s2 + done * S, take * S, rb->st_s2.data() + rb->st_n * S * es);
+    to_ring(rb, r + done, take, rb->st_r.data() + rb->st_n * es);
+    memcpy(rb->st_a.data() + rb->st_n * A, a + done * A, take * A * 4);
+    for (int i = 0; i < take; ++i) rb->st_t[rb->st_n + i] = t[done + i] ? 1.f : 0.f;
+    rb->st_n += take;
+    rb->total += take;
+    rb->count = std::min<int64_t>(rb->total, rb->cap);
+    done += take;
+    if (rb->st_n == kStageRows) replay_flush(rb);
+  }
+}
+}  // extern "C++"
+
 int ddpg_replay_add(ddpg_replay* rb, const float* s, const float* a, const float* r,
                     const uint8_t* t, const float* s2, int n) {
-  return rguard(rb, [&] {
-    if (n < 0) throw einval("negative row count");
-    HIP_TRY(hipSetDevice(rb->device));
-    const size_t S = rb->S, A = rb->A;
-    int done = 0;
-    if (n >= kStageRows) {  // bulk insert: straight from the caller's arrays
-      replay_flush(rb);
-      if (rb->last_read) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->last_read, 0));
-      std::vector<float> rf(r, r + n), tf(n);
-      for (int i = 0; i < n; ++i) tf[i] = t[i] ? 1.f : 0.f;
-      // only the last `cap` rows can survive; skip the ones that would be overwritten
-      const int64_t skip = n > rb->cap ? n - rb->cap : 0;
-      ring_write(rb, rb->total + skip, (int)(n - skip), s + skip * S, a + skip * A, rf.data() + skip,
-                 tf.data() + skip, s2 + skip * S);
-      HIP_TRY(hipStreamSynchronize(rb->stream));
-      rb->total += n;
-      rb->count = std::min<int64_t>(rb->total, rb->cap);
-      return;
-    }
-    while (done < n) {
-      if (rb->st_n == 0) rb->st_first = rb->total;
-      const int take = std::min(n - done, kStageRows - rb->st_n);
-      memcpy(rb->st_s.data() + rb->st_n * S, s + done * S, take * S * 4);
-      memcpy(rb->st_s2.data() + rb->st_n * S, s2 + done * S, take * S * 4);
-      memcpy(rb->st_a.data() + rb->st_n * A, a + done * A, take * A * 4);
-      for (int i = 0; i < take; ++i) {
-        rb->st_r[rb->st_n + i] = r[done + i];
-        rb->st_t[rb->st_n + i] = t[done + i] ? 1.f : 0.f;
-      }
-      rb->st_n += take;
-      rb->total += take;
-      rb->count = std::min<int64_t>(rb->total, rb->cap);
-      done += take;
-      if (rb->st_n == kStageRows) replay_flush(rb);
-    }
-  });
+  return rguard(rb, [&] { replay_add_impl<float>(rb, s, a, r, t, s2, n); });
+}
+
+int ddpg_replay_add_f64(ddpg_replay* rb, const double* s, const float* a, const double* r,
+                        const uint8_t* t, const double* s2, int n) {
+  return rguard(rb, [&] { replay_add_impl<double>(rb, s, a, r, t, s2, n); });
 }
 
 int64_t ddpg_replay_size(ddpg_replay* rb) { return rb ? rb->count : 0; }
@@ -1765,8 +1858,13 @@ static inline int pos_to_slot(const ddpg_replay* rb, int64_t pos) {
   return (int)((rb->total - rb->count + pos) % rb->cap);
 }
 
-int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* r, uint8_t* t,
-                             float* s2, int64_t* idx_out) {
+extern "C++" {
+// ReplayBuffer.sample_batch to host arrays of type T (s, s2, r).  The rows are
+// gathered on device in the ring's own precision (byte copies) and converted
+// on the host: exact for a float64 ring read as float64 and for a fp32 ring.
+template <class T>
+static int sample_impl(ddpg_replay* rb, int B, T* s, float* a, T* r, uint8_t* t, T* s2,
+                       int64_t* idx_out) {
   int got = 0;
   int rc = rguard(rb, [&] {
     if (B < 0) throw einval("negative batch");
@@ -1780,47 +1878,80 @@ int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* 
     if (k == 0) return;
     rb->tmp_slot.resize(k);
     for (int i = 0; i < k; ++i) rb->tmp_slot[i] = pos_to_slot(rb, rb->tmp_idx[i]);
-    const int S = rb->S, A = rb->A;
+    const size_t S = rb->S, A = rb->A, es = rb->es();
     if (rb->d_slots_cap < k) {
       if (rb->d_slots) HIP_TRY(hipFree(rb->d_slots));
       HIP_TRY(hipMalloc(&rb->d_slots, k * sizeof(int)));
       rb->d_slots_cap = k;
     }
-    const size_t need = (size_t)k * (2 * S + A + 2);
+    const size_t row_bytes = 2 * S * es + A * 4 + es + 4;
+    const size_t need = (size_t)k * row_bytes;
     if (rb->d_tmp_cap < need) {
       if (rb->d_tmp) HIP_TRY(hipFree(rb->d_tmp));
-      HIP_TRY(hipMalloc(&rb->d_tmp, need * 4));
+      HIP_TRY(hipMalloc(&rb->d_tmp, need));
       rb->d_tmp_cap = need;
     }
-    float* ds = rb->d_tmp;
-    float* ds2 = ds + (size_t)k * S;
-    float* da = ds2 + (size_t)k * S;
-    float* dr = da + (size_t)k * A;
-    float* dt = dr + k;
+    // output planes, each [k][row bytes]: s | s2 | a | r | t
+    unsigned char* o_s = rb->d_tmp;
+    unsigned char* o_s2 = o_s + k * S * es;
+    unsigned char* o_a = o_s2 + k * S * es;
+    unsigned char* o_r = o_a + k * A * 4;
+    unsigned char* o_t = o_r + k * es;
     HIP_TRY(hipMemcpyAsync(rb->d_slots, rb->tmp_slot.data(), k * sizeof(int),
                            hipMemcpyHostToDevice, rb->stream));
-    hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(k, 4)), dim3(256), 0, rb->stream,
-                       rb->d_slots, k, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, S, A, ds, ds2, S,
-                       da, A, dr, dt, nullptr, nullptr);
-    HIP_TRY(hipGetLastError());
-    std::vector<float> tmp(need);
-    HIP_TRY(hipMemcpyAsync(tmp.data(), rb->d_tmp, need * 4, hipMemcpyDeviceToHost, rb->stream));
+    struct Plane {
+      const unsigned char* src;
+      unsigned char* dst;
+      size_t bytes;
+    } planes[5] = {{rb->ps(), o_s, S * es},
+                   {rb->ps2(), o_s2, S * es},
+                   {(const unsigned char*)rb->ra, o_a, A * 4},
+                   {rb->pr(), o_r, es},
+                   {(const unsigned char*)rb->rt, o_t, 4}};
+    for (const Plane& pl : planes) {
+      hipLaunchKernelGGL(gather_bytes_kernel, dim3(std::min(ceil_div(k, 4), 4096)), dim3(256), 0,
+                         rb->stream, rb->d_slots, k, pl.src, pl.dst, (long long)pl.bytes);
+      HIP_TRY(hipGetLastError());
+    }
+    std::vector<unsigned char> tmp(need);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), rb->d_tmp, need, hipMemcpyDeviceToHost, rb->stream));
     HIP_TRY(hipStreamSynchronize(rb->stream));
-    if (s) memcpy(s, tmp.data(), (size_t)k * S * 4);
-    if (s2) memcpy(s2, tmp.data() + (size_t)k * S, (size_t)k * S * 4);
-    if (a) memcpy(a, tmp.data() + (size_t)2 * k * S, (size_t)k * A * 4);
-    if (r) memcpy(r, tmp.data() + (size_t)k * (2 * S + A), (size_t)k * 4);
+    auto conv = [&](const unsigned char* src, size_t n, T* dst) {
+      if (!dst) return;
+      if (rb->f64)
+        for (size_t i = 0; i < n; ++i) dst[i] = (T)((const double*)src)[i];
+      else
+        for (size_t i = 0; i < n; ++i) dst[i] = (T)((const float*)src)[i];
+    };
+    const size_t off_s2 = k * S * es, off_a = 2 * off_s2, off_r = off_a + k * A * 4,
+                 off_t = off_r + k * es;
+    conv(tmp.data(), k * S, s);
+    conv(tmp.data() + off_s2, k * S, s2);
+    conv(tmp.data() + off_r, k, r);
+    if (a) memcpy(a, tmp.data() + off_a, (size_t)k * A * 4);
     if (t)
-      for (int i = 0; i < k; ++i) t[i] = tmp[(size_t)k * (2 * S + A + 1) + i] != 0.f;
+      for (int i = 0; i < k; ++i) t[i] = ((const float*)(tmp.data() + off_t))[i] != 0.f;
   });
   return rc == DDPG_OK ? got : rc;
+}
+}  // extern "C++"
+
+int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* r, uint8_t* t,
+                             float* s2, int64_t* idx_out) {
+  return sample_impl<float>(rb, B, s, a, r, t, s2, idx_out);
+}
+
+int ddpg_replay_sample_batch_f64(ddpg_replay* rb, int B, double* s, float* a, double* r,
+                                 uint8_t* t, double* s2, int64_t* idx_out) {
+  return sample_impl<double>(rb, B, s, a, r, t, s2, idx_out);
 }
 
 // ---------------------------------------------------------------- fused step
 static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
   ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
   hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->cur,
-                     c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, c->S, c->A, c->s,
+                     c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, rb->rsd, rb->rs2d,
+                     rb->rrd, c->S, c->A, c->s,
                      c->s2, c->ldS, c->a, c->ldA, c->r, c->t, c->has_scaler ? c->dmean : nullptr,
                      c->has_scaler ? c->dscale : nullptr);
   HIP_TRY(hipGetLastError());
@@ -1877,6 +2008,9 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     learner_step_any(c, rb, B, inv_b);
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
+  // a large-path step (eager, or a graph replay that captured no host flag
+  // update) moved theta without refreshing the small path's W^T shadows
+  if (!(c->sb_ok && c->world == 1 && B <= c->sb_max_b)) c->sb_shadow_ok = false;
   if (stats) {
     float st[2];
     HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));
@@ -1941,6 +2075,7 @@ int ddpg_comm_init(ddpg_ctx* c, const char* id128, int world, int rank) {
     ncclUniqueId id;
     memcpy(&id, id128, 128);
     HIP_TRY(hipSetDevice(c->cfg.device));
+    if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)world * sizeof(float)));
     ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
     if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
   });

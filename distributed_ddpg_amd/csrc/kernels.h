@@ -11,11 +11,16 @@ namespace ddpg {
 // ---------------------------------------------------------------- K8 gather
 // replay_buffer.py:41-45 (np.array stacking of the sampled tuples), from a
 // device-resident SoA ring.  One wave per row; lanes stride the features.
-// Optional scaler (networks.py:65-69): fp32((double(x) - mean) / scale).
+// A float64 ring (rsd / rs2d / rrd non-null) keeps the states and rewards the
+// reference stores; they are rounded to fp32 here, once, like TF's feed_dict.
+// Optional scaler (networks.py:65-69, ddpg.py:184-189), applied to replay
+// rows only: fp32((double(x) - mean) / scale).
 __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
                                    const float* __restrict__ rs, const float* __restrict__ ra,
                                    const float* __restrict__ rr, const float* __restrict__ rt,
-                                   const float* __restrict__ rs2, int S, int A,
+                                   const float* __restrict__ rs2, const double* __restrict__ rsd,
+                                   const double* __restrict__ rs2d,
+                                   const double* __restrict__ rrd, int S, int A,
                                    float* __restrict__ s, float* __restrict__ s2, int lds,
                                    float* __restrict__ a, int lda, float* __restrict__ r,
                                    float* __restrict__ t, const double* __restrict__ mean,
@@ -25,34 +30,65 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   for (int b = wave; b < B; b += nwaves) {
     const size_t slot = (size_t)slots[b];
-    const float* ps = rs + slot * S;
-    const float* ps2 = rs2 + slot * S;
     for (int j = lane; j < S; j += 64) {
-      float x = ps[j], x2 = ps2[j];
-      if (mean) {
-        x = (float)(((double)x - mean[j]) / scale[j]);
-        x2 = (float)(((double)x2 - mean[j]) / scale[j]);
+      const size_t e = slot * S + j;
+      float x, x2;
+      if (rsd) {
+        const double xd = rsd[e], x2d = rs2d[e];
+        x = mean ? (float)((xd - mean[j]) / scale[j]) : (float)xd;
+        x2 = mean ? (float)((x2d - mean[j]) / scale[j]) : (float)x2d;
+      } else {
+        x = rs[e];
+        x2 = rs2[e];
+        if (mean) {
+          x = (float)(((double)x - mean[j]) / scale[j]);
+          x2 = (float)(((double)x2 - mean[j]) / scale[j]);
+        }
       }
       s[(size_t)b * lds + j] = x;
       s2[(size_t)b * lds + j] = x2;
     }
     for (int j = lane; j < A; j += 64) a[(size_t)b * lda + j] = ra[slot * A + j];
     if (lane == 0) {
-      r[b] = rr[slot];
+      r[b] = rrd ? (float)rrd[slot] : rr[slot];
       t[b] = rt[slot];
     }
   }
 }
 
-// Apply the scaler in place to a [B][ld] state buffer (1:1 API path).
-__global__ void scale_rows_kernel(float* __restrict__ x, int B, int S, int ld,
-                                  const double* __restrict__ mean,
-                                  const double* __restrict__ scale) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * S) return;
-  const int b = i / S, j = i - b * S;
-  float* p = x + (size_t)b * ld + j;
-  *p = (float)(((double)*p - mean[j]) / scale[j]);
+// Row gather of one ring plane as raw 32-bit words (host sample_batch path:
+// the rows keep the ring's precision; row_bytes is a multiple of 4).
+__global__ void gather_bytes_kernel(const int* __restrict__ slots, int B,
+                                    const unsigned char* __restrict__ src,
+                                    unsigned char* __restrict__ dst, long long row_bytes) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const long long words = row_bytes >> 2;
+  for (int b = wave; b < B; b += nwaves) {
+    const unsigned* ps = (const unsigned*)(src + (size_t)slots[b] * row_bytes);
+    unsigned* pd = (unsigned*)(dst + (size_t)b * row_bytes);
+    for (long long j = lane; j < words; j += 64) pd[j] = ps[j];
+  }
+}
+
+// Data-parallel stats (world > 1): all[w] = rank w's {q_max, loss share};
+// max and an ordered sum, identical on every rank.
+__global__ void stats_reduce_kernel(const float* __restrict__ all, int world,
+                                    float* __restrict__ stats, double* __restrict__ acc) {
+  if (threadIdx.x != 0) return;
+  float qm = all[0], ls = all[1];
+  for (int w = 1; w < world; ++w) {
+    qm = fmaxf(qm, all[2 * w]);
+    ls = __fadd_rn(ls, all[2 * w + 1]);
+  }
+  stats[0] = qm;
+  stats[1] = ls;
+  if (acc) {
+    acc[0] += (double)qm;
+    acc[1] += (double)ls;
+    acc[2] += 1.0;
+  }
 }
 
 // ---------------------------------------------------------------- thin heads

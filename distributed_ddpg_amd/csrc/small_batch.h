@@ -86,7 +86,9 @@ struct SbArgs {
   // replay ring + this step's slots (fused gather)
   const int* slots;
   const float *rs, *ra, *rr, *rt, *rs2;
-  const double *mean, *sdev;  // optional scaler
+  const double *rsd, *rs2d, *rrd;  // float64 ring planes (s, s2, r) when the ring keeps them
+  const double *mean, *sdev;  // optional scaler (applied to replay rows only)
+  float* grad;           // flat gradient buffer (written for ddpg_get_params readback)
   float* theta;
   float* target;
   float* adam_m;
@@ -370,9 +372,12 @@ DDPG_DEV void sb_alpha_and_advance(float* pw, float* alpha, float lr, float b1, 
 }
 
 // dst[k][r] = ring[slot(r0 + r)][k] for k < cols, zero up to ldk features and
-// for rows past `valid`; the scaler (x - mean) / scale in fp64 when mean.
+// for rows past `valid`; read from the float64 plane `ringd` when the ring
+// keeps one; the scaler (x - mean) / scale in fp64 when mean, then one
+// rounding to fp32 (the reference's preprocess_input + feed_dict cast).
 // save (optional): the valid rows also go to save[k * Bp + r0 + r].
-DDPG_DEV void sb_gather(lds_f* dst, int ldk, const float* __restrict__ ring, int cols,
+DDPG_DEV void sb_gather(lds_f* dst, int ldk, const float* __restrict__ ring,
+                        const double* __restrict__ ringd, int cols,
                         const int* __restrict__ slots, int r0, int valid,
                         const double* __restrict__ mean, const double* __restrict__ sdev,
                         float* __restrict__ save, int Bp) {
@@ -380,8 +385,9 @@ DDPG_DEV void sb_gather(lds_f* dst, int ldk, const float* __restrict__ ring, int
     const int k = idx >> 2, r = idx & 3;
     float x = 0.f;
     if (r < valid && k < cols) {
-      x = ring[(size_t)slots[r0 + r] * cols + k];
-      if (mean) x = (float)(((double)x - mean[k]) / sdev[k]);
+      const size_t e = (size_t)slots[r0 + r] * cols + k;
+      const double xd = ringd ? ringd[e] : (double)ring[e];
+      x = mean ? (float)((xd - mean[k]) / sdev[k]) : (float)xd;
       if (save) save[(size_t)k * Bp + r0 + r] = x;
     }
     dst[idx] = x;
@@ -420,13 +426,14 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   SB_STAMP(0);
 
   if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw + 2, g.alpha + 1, g.lr_c, g.b1, g.b2);
-  sb_gather(xs, LX, g.rs, g.S, g.slots, r0, valid, g.mean, g.sdev, g.sv.xs, g.sv.Bp);
-  sb_gather(xs2, LX, g.rs2, g.S, g.slots, r0, valid, g.mean, g.sdev, nullptr, 0);
-  sb_gather(xa, LX, g.ra, g.A, g.slots, r0, valid, nullptr, nullptr, g.sv.xa, g.sv.Bp);
+  sb_gather(xs, LX, g.rs, g.rsd, g.S, g.slots, r0, valid, g.mean, g.sdev, g.sv.xs, g.sv.Bp);
+  sb_gather(xs2, LX, g.rs2, g.rs2d, g.S, g.slots, r0, valid, g.mean, g.sdev, nullptr, 0);
+  sb_gather(xa, LX, g.ra, nullptr, g.A, g.slots, r0, valid, nullptr, nullptr, g.sv.xa, g.sv.Bp);
   if (tid < 4) {
     const bool ok = tid < valid;
-    col[4 * 4 + tid] = ok ? g.rr[g.slots[r0 + tid]] : 0.f;
-    col[5 * 4 + tid] = ok ? g.rt[g.slots[r0 + tid]] : 0.f;
+    const int sl = ok ? g.slots[r0 + tid] : 0;
+    col[4 * 4 + tid] = ok ? (g.rrd ? (float)g.rrd[sl] : g.rr[sl]) : 0.f;
+    col[5 * 4 + tid] = ok ? g.rt[sl] : 0.f;
   }
   __syncthreads();
   SB_STAMP(1);
@@ -617,10 +624,8 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
   for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
     const int k = idx >> 2, r = idx & 3;
     float x = 0.f;
-    if (r < valid && k < g.S) {
-      x = in.s[(r0 + r) * g.S + k];
-      if (g.mean) x = (float)(((double)x - g.mean[k]) / g.sdev[k]);
-    }
+    // states arrive preprocessed (the caller's preprocess_input): no scaler here
+    if (r < valid && k < g.S) x = in.s[(r0 + r) * g.S + k];
     xs[idx] = x;
   }
   __syncthreads();
@@ -712,6 +717,7 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     g.adam_m[i] = m;
     g.adam_v[i] = v;
     g.theta[i] = p;
+    g.grad[i] = gv;
     g.target[i] = __fadd_rn(__fmul_rn(p, g.tau), __fmul_rn(t0, g.omt));
     if (ti == tab.shadow) tab.sh[(size_t)n * T.K + k] = p;
   }

@@ -12,7 +12,7 @@ apply asynchronous Hogwild updates on the PS; that semantics is deliberately
 replaced (DESIGN.md).
 
 Per environment step the worker does what ddpg.py:66-116 does: act with
-actor.predict(s) + 1/(1+episode), store the transition, and -- once the
+actor.predict(s) + 1/(1+global_step), store the transition, and -- once the
 buffer holds more than batch_size rows -- one learner update (the fused
 device path, ddpg_learner_step).  gym/MuJoCo are used when importable; this
 image has neither, so --env synthetic (default when gym is missing) provides
@@ -92,23 +92,49 @@ def run_ps(opt):
         time.sleep(3600)
 
 
+def rendezvous(opt, rank):
+    """Join the ps-hosted store as worker `rank` of len(opt.workers) and form
+    the gloo group the RCCL unique id travels over (the reference's
+    ClusterSpec + Server, ddpg.py:168-174).  Returns the world size."""
+    import torch.distributed as dist
+    from torch.distributed import TCPStore
+    world = len(opt.workers)
+    if world > 1:
+        host, port = _host_port(opt.parameter_servers[0])
+        store = TCPStore(host, port, world_size=world + 1, is_master=False)
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
+    return world
+
+
+def rendezvous_check(opt, rank):
+    """--rendezvous_only: the launch path up to the unique-id exchange without
+    a GPU.  Rank 0 broadcasts a 128-byte id (random bytes standing in for
+    ncclGetUniqueId, which needs the HIP runtime) over the gloo group exactly
+    as learner.init_comm does; every rank then reports the id it received."""
+    import torch.distributed as dist
+    world = rendezvous(opt, rank)
+    obj = [os.urandom(128) if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0)
+        ids = [None] * world
+        dist.all_gather_object(ids, obj[0])
+        assert all(i == obj[0] for i in ids), "unique id differs across ranks"
+        dist.destroy_process_group()
+    print("rendezvous ok rank %d of %d id %s" % (rank, world, obj[0][:8].hex()), flush=True)
+
+
 def run_worker(opt, task_index, env_name, episodes, device):
     import torch
     import torch.distributed as dist
-    from torch.distributed import TCPStore
 
     from . import checkpoint, networks as nets, summary
     from .learner import FusedLearner, init_comm
     from .replay_buffer import ReplayBuffer
 
-    world = len(opt.workers)
     rank = task_index
     np.random.seed(opt.seed)
     torch.cuda.set_device(device)
-    if world > 1:
-        host, port = _host_port(opt.parameter_servers[0])
-        store = TCPStore(host, port, world_size=world + 1, is_master=False)
-        dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
+    world = rendezvous(opt, rank)
 
     env = make_env(env_name, opt.seed + rank)
     scaler = None
@@ -154,7 +180,9 @@ def run_worker(opt, task_index, env_name, episodes, device):
     ep_reward, ep_q, ep_loss = 0.0, 0.0, 0.0
     solved = False
     while True:
-        a = actor.predict(np.reshape(state, (1, S))) + (1.0 / (1.0 + episode))
+        # exploration offset 1/(1 + global_step): global_step is the episode
+        # counter restored from the checkpoint (ddpg.py:69, 250)
+        a = actor.predict(np.reshape(state, (1, S))) + (1.0 / (1.0 + global_step))
         state2, r, done, _ = env.step(a[0])
         replay.add(np.reshape(state, (S,)), np.reshape(a, (A,)), r, done,
                    np.reshape(state2, (S,)))
@@ -168,10 +196,14 @@ def run_worker(opt, task_index, env_name, episodes, device):
         if done:
             stats.append(ep_reward)
             if is_chief:  # ddpg.py:118-127
-                writer.add_episode(global_step, ep_reward, ep_q / max(t, 1), ep_loss / max(t, 1))
+                # the reference divides by its 0-based step index at `done`
+                # (steps - 1); a one-step episode would divide by zero there,
+                # so that case divides by 1
+                div = float(max(t - 1, 1))
+                writer.add_episode(global_step, ep_reward, ep_q / div, ep_loss / div)
                 writer.flush()
                 print("Episode: %d - Iterations: %d - Reward: %f - Qmax: %f - Loss: %f" % (
-                    global_step, t, ep_reward, ep_q / max(t, 1), ep_loss / max(t, 1)), flush=True)
+                    global_step, t - 1, ep_reward, ep_q / div, ep_loss / div), flush=True)
             if np.mean(stats[-100:]) > 950 and len(stats) >= 101:  # ddpg.py:255-260
                 print(np.mean(stats[-100:]))
                 print("Solved.")
@@ -210,13 +242,21 @@ def main(argv=None):
     ap.add_argument("--device", type=int, default=None)
     ap.add_argument("--workers", default=None,
                     help="comma-separated worker addresses (default Parameters.workers)")
+    ap.add_argument("--ps", default=None,
+                    help="parameter-server (rendezvous) address (default Parameters.parameter_servers[0])")
+    ap.add_argument("--rendezvous_only", action="store_true",
+                    help="worker: join the group, exchange the unique id, exit (no GPU)")
     args = ap.parse_args(argv)
     opt = Parameters()
     if args.workers:
         opt.workers = args.workers.split(",")
         opt.num_workers = len(opt.workers)
+    if args.ps:
+        opt.parameter_servers = [args.ps]
     if args.job_name == "ps":
         run_ps(opt)
+    elif args.job_name == "worker" and args.rendezvous_only:
+        rendezvous_check(opt, args.task_index)
     elif args.job_name == "worker":
         env = args.env or opt.env_name
         run_worker(opt, args.task_index, env, args.episodes or opt.max_episodes,

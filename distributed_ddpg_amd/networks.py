@@ -147,7 +147,7 @@ class Session:
         check(lib.ddpg_get_params(self.ctx, which, fptr(out), n), self.ctx)
         if not split:
             return out
-        shapes = self.actor.shapes() if which in (0, 1, 4, 5) else self.critic.shapes()
+        shapes = self.actor.shapes() if which in (0, 1, 4, 5, 8) else self.critic.shapes()
         res, o = [], 0
         for s in shapes:
             k = int(np.prod(s))

@@ -7,10 +7,14 @@ Differences from the reference, by design:
     `random` module (the reference seeds the global RNG at replay_buffer.py:19;
     nothing else in the learner path draws from it, so the index stream is
     identical);
-  * rows are stored in fp32 -- the precision at which the reference's
-    networks consume them (TF feed_dict casts); sample_batch returns s, r, s2
-    as float64 views of those values and t as bool, like np.array stacking of
-    the reference's tuples;
+  * the ring's precision follows the first rows added, as the reference's
+    deque keeps whatever it is given: float64 states (what gym envs emit) give
+    a float64 ring (s, s2, r kept exactly; sample_batch returns the stored
+    values and the fused step applies the scaler to the unrounded state, then
+    rounds once, like preprocess_input + feed_dict); float32 rows give a
+    float32 ring (half the HBM; the bench's synthetic rows).  sample_batch
+    returns s, r, s2 as float64 and t as bool, like np.array stacking of the
+    reference's tuples;
   * clear() works (the reference's references a non-existent self.deque).
 """
 import ctypes
@@ -27,16 +31,19 @@ class ReplayBuffer:
         self.random_seed = int(random_seed)
         self.device = int(device)
         self.count = 0
-        self._rb = None  # created on first add, when the row dims are known
+        self._rb = None  # created on first add, when the row dims and precision are known
         self.s_dim = self.a_dim = None
+        self.f64 = False
 
     # -- internals
-    def _ensure(self, s_dim, a_dim):
+    def _ensure(self, s_dim, a_dim, f64):
         if self._rb is None:
             self._rb = ctypes.c_void_p()
-            check(lib.ddpg_replay_create(self.device, s_dim, a_dim, self.buffer_size,
-                                         self.random_seed, ctypes.byref(self._rb)))
+            check(lib.ddpg_replay_create_ex(self.device, s_dim, a_dim, self.buffer_size,
+                                            self.random_seed, _lib.REPLAY_F64 if f64 else 0,
+                                            ctypes.byref(self._rb)))
             self.s_dim, self.a_dim = s_dim, a_dim
+            self.f64 = bool(f64)
         elif (s_dim, a_dim) != (self.s_dim, self.a_dim):
             raise ValueError("row dims changed: (%d,%d) -> (%d,%d)" % (
                 self.s_dim, self.a_dim, s_dim, a_dim))
@@ -53,22 +60,34 @@ class ReplayBuffer:
 
     # -- reference interface
     def add(self, s, a, r, t, s2):
-        s = np.asarray(s, np.float32).reshape(1, -1)
-        a = np.asarray(a, np.float32).reshape(1, -1)
-        self.add_batch(s, a, np.array([r], np.float32), np.array([bool(t)]),
-                       np.asarray(s2, np.float32).reshape(1, -1))
+        """replay_buffer.py:21-28 (one transition)."""
+        s = np.asarray(s)
+        f64 = s.dtype == np.float64 if self._rb is None else self.f64
+        dt = np.float64 if f64 else np.float32
+        self.add_batch(np.asarray(s, dt).reshape(1, -1), np.asarray(a, np.float32).reshape(1, -1),
+                       np.array([r], dt), np.array([bool(t)]),
+                       np.asarray(s2, dt).reshape(1, -1))
 
     def add_batch(self, s, a, r, t, s2):
-        s = np.ascontiguousarray(s, np.float32)
+        """n transitions at once (rows of s, a, r, t, s2)."""
+        s = np.asarray(s)
+        f64 = s.dtype == np.float64 if self._rb is None else self.f64
+        dt = np.float64 if f64 else np.float32
+        s = np.ascontiguousarray(s, dt)
+        s2 = np.ascontiguousarray(s2, dt)
         a = np.ascontiguousarray(a, np.float32)
-        s2 = np.ascontiguousarray(s2, np.float32)
         n = s.shape[0]
-        r = np.ascontiguousarray(np.asarray(r, np.float32).reshape(n))
+        r = np.ascontiguousarray(np.asarray(r, dt).reshape(n))
         t = np.ascontiguousarray(np.asarray(t).reshape(n).astype(np.uint8))
-        self._ensure(s.shape[1], a.shape[1])
-        self._err(lib.ddpg_replay_add(self._rb, _lib.fptr(s), _lib.fptr(a), _lib.fptr(r),
-                                      t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
-                                      _lib.fptr(s2), n))
+        self._ensure(s.shape[1], a.shape[1], f64)
+        u8 = t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        if f64:
+            rc = lib.ddpg_replay_add_f64(self._rb, _lib.dptr(s), _lib.fptr(a), _lib.dptr(r), u8,
+                                         _lib.dptr(s2), n)
+        else:
+            rc = lib.ddpg_replay_add(self._rb, _lib.fptr(s), _lib.fptr(a), _lib.fptr(r), u8,
+                                     _lib.fptr(s2), n)
+        self._err(rc)
         self.count = int(lib.ddpg_replay_size(self._rb))
 
     def size(self):
@@ -80,18 +99,16 @@ class ReplayBuffer:
             return (empty, empty, empty, empty.astype(bool), empty)
         k = min(int(batch_size), self.count)
         S, A = self.s_dim, self.a_dim
-        s = np.empty((max(k, 1), S), np.float32)
-        s2 = np.empty((max(k, 1), S), np.float32)
-        a = np.empty((max(k, 1), A), np.float32)
-        r = np.empty(max(k, 1), np.float32)
-        t = np.empty(max(k, 1), np.uint8)
-        idx = np.empty(max(k, 1), np.int64)
-        got = self._err(lib.ddpg_replay_sample_batch(
-            self._rb, int(batch_size), _lib.fptr(s), _lib.fptr(a), _lib.fptr(r),
-            t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _lib.fptr(s2),
+        n = max(k, 1)
+        s, s2, r = np.empty((n, S)), np.empty((n, S)), np.empty(n)
+        a = np.empty((n, A), np.float32)
+        t = np.empty(n, np.uint8)
+        idx = np.empty(n, np.int64)
+        got = self._err(lib.ddpg_replay_sample_batch_f64(
+            self._rb, int(batch_size), _lib.dptr(s), _lib.fptr(a), _lib.dptr(r),
+            t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _lib.dptr(s2),
             idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
-        out = (s[:got].astype(np.float64), a[:got], r[:got].astype(np.float64),
-               t[:got].astype(bool), s2[:got].astype(np.float64))
+        out = (s[:got], a[:got], r[:got], t[:got].astype(bool), s2[:got])
         if return_indices:
             return out + (idx[:got],)
         return out

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DDPG_ABI_VERSION 1
+#define DDPG_ABI_VERSION 2
 
 enum ddpg_status {
   DDPG_OK = 0,
@@ -53,8 +53,16 @@ enum ddpg_which {
   DDPG_ACTOR_ADAM_M = 4,  /* "<var>/Adam"   slots of the actor optimiser */
   DDPG_ACTOR_ADAM_V = 5,  /* "<var>/Adam_1" */
   DDPG_CRITIC_ADAM_M = 6,
-  DDPG_CRITIC_ADAM_V = 7
+  DDPG_CRITIC_ADAM_V = 7,
+  /* get only: the gradient the last update applied (after the data-parallel
+   * sum), i.e. the `grads` of networks.py:44 / the compute_gradients of
+   * networks.py:137, in the same flat order */
+  DDPG_ACTOR_GRAD = 8,
+  DDPG_CRITIC_GRAD = 9
 };
+
+/* ddpg_replay_create_ex flags */
+#define DDPG_REPLAY_F64 1  /* keep s, s2, r as float64 (the reference's deque values) */
 
 /* soft-update mask (ddpg_soft_update) */
 #define DDPG_SOFT_ACTOR 1
@@ -124,7 +132,11 @@ int ddpg_actor_train(ddpg_ctx* ctx, const float* s, const float* a_gradient, int
 /* update_target_network (mask: DDPG_SOFT_*)        networks.py:34-37,87-88,126-128,195-196 */
 int ddpg_soft_update(ddpg_ctx* ctx, int mask);
 /* per-feature affine input scaler (sklearn StandardScaler.transform, ddpg.py:184-189,
- * networks.py:65-69,164-168); applied in float64 then rounded to fp32.  NULL clears. */
+ * networks.py:65-69,164-168): (x - mean) / scale in float64, then one rounding to
+ * fp32.  Applied ONLY where the library reads raw replay rows (the fused
+ * learner step's gathers).  The 1:1 methods above take states that the caller
+ * already preprocessed (the shims' preprocess_input, float64 on the host), as
+ * the reference's feed_dict received them.  NULL clears. */
 int ddpg_set_scaler(ddpg_ctx* ctx, const double* mean, const double* scale, int S);
 
 /* ------------------------------------------------------------- replay */
@@ -139,14 +151,24 @@ int ddpg_sampler_sample(ddpg_sampler* s, int64_t n, int k, int64_t* out);
 int ddpg_sampler_getrandbits32(ddpg_sampler* s, uint32_t* out, int n);
 
 /* Device ring buffer of transitions (ReplayBuffer replay_buffer.py:10-51).
- * Rows: s[S], a[A], r, t, s2[S] stored fp32 (t as 0/1). */
+ * Rows: s[S], a[A], r, t, s2[S]; a fp32, t as 0/1; s, s2, r fp32, or float64
+ * with DDPG_REPLAY_F64 (what the reference's deque holds when the env emits
+ * float64 states: sample_batch then returns them exactly and the scaler sees
+ * the unrounded state).  The learner rounds them to fp32 once, as TF's
+ * feed_dict does. */
 int ddpg_replay_create(int device, int state_dim, int action_dim, int64_t capacity,
                        int64_t seed, ddpg_replay** out);
+int ddpg_replay_create_ex(int device, int state_dim, int action_dim, int64_t capacity,
+                          int64_t seed, int flags, ddpg_replay** out);
+int ddpg_replay_is_f64(ddpg_replay* rb);
 void ddpg_replay_destroy(ddpg_replay* rb);
 const char* ddpg_replay_last_error(ddpg_replay* rb);
 /* ReplayBuffer.add (replay_buffer.py:21-28), n rows at once (host arrays) */
 int ddpg_replay_add(ddpg_replay* rb, const float* s, const float* a, const float* r,
                     const uint8_t* t, const float* s2, int n);
+/* the same with float64 s, r, s2 (rounded to fp32 when the ring is fp32) */
+int ddpg_replay_add_f64(ddpg_replay* rb, const double* s, const float* a, const double* r,
+                        const uint8_t* t, const double* s2, int n);
 /* ReplayBuffer.size (replay_buffer.py:30-31) */
 int64_t ddpg_replay_size(ddpg_replay* rb);
 int64_t ddpg_replay_total_added(ddpg_replay* rb);
@@ -158,6 +180,9 @@ int ddpg_replay_clear(ddpg_replay* rb);
  * the deque positions. */
 int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* r,
                              uint8_t* t, float* s2, int64_t* idx_out);
+/* the same with float64 s, r, s2 outputs (exact for a DDPG_REPLAY_F64 ring) */
+int ddpg_replay_sample_batch_f64(ddpg_replay* rb, int B, double* s, float* a, double* r,
+                                 uint8_t* t, double* s2, int64_t* idx_out);
 
 /* ------------------------------------------------------------- fused path */
 /* One whole learner step, ddpg.py:86-113, on device: sample (host MT19937)
@@ -165,7 +190,9 @@ int ddpg_replay_sample_batch(ddpg_replay* rb, int B, float* s, float* a, float* 
  * critic train (K2,K3,K6) -> actor fwd + dQ/da (K1,K4) -> actor train
  * (K5,K6) -> both soft updates (K7).  B is the GLOBAL batch; with world>1
  * this rank processes rows [rank*B/world, (rank+1)*B/world) and gradients
- * are summed over ranks with RCCL.  stats may be NULL (no host sync). */
+ * are summed over ranks with RCCL; with a communicator the stats are the
+ * global-batch ones (max over ranks of max(Q), sum of the loss shares).
+ * stats may be NULL (no host sync). */
 int ddpg_learner_step(ddpg_ctx* ctx, ddpg_replay* rb, int B, ddpg_stats* stats);
 /* Same, with an explicit host index list (deque positions, length B). */
 int ddpg_learner_step_indices(ddpg_ctx* ctx, ddpg_replay* rb, const int64_t* idx, int B,

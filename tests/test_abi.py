@@ -37,7 +37,7 @@ def test_nm_dynamic_exports():
 
 def test_abi_version_and_errors_without_gpu():
     from distributed_ddpg_amd import _lib
-    assert _lib.lib.ddpg_abi_version() == 1
+    assert _lib.lib.ddpg_abi_version() == _lib.ABI_VERSION == 2
     # creating a context with bad dims fails cleanly (no exception crosses the ABI)
     cfg = _lib.Cfg()
     h = _lib.ctypes.c_void_p()

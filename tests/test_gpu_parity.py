@@ -54,6 +54,8 @@ def dd():
 CONFIGS = {
     # name: S, A, H1, H2, scale, B, source  (critic widths in CRITIC_W when they differ)
     "ip": (4, 1, 128, 200, 3.0, 64, "ip_model1410"),
+    # C2 at the reference's default batch (parameters.py:11)
+    "ip256": (4, 1, 128, 200, 3.0, 256, "ip_model1410"),
     "mc": (2, 1, 48, 64, 1.0, 64, "mc_model120"),
     "odd": (5, 3, 40, 72, 2.0, 37, None),
     "wide": (64, 16, 1024, 1024, 1.0, 256, None),
@@ -300,7 +302,7 @@ def test_replay_device_sample_bitexact(dd):
                 j += 1
 
 
-@pytest.mark.parametrize("name", ["ip", "odd", "wide"])
+@pytest.mark.parametrize("name", ["ip", "ip256", "odd", "wide"])
 def test_fused_learner_step_parity(dd, O, name):
     """ddpg_learner_step (sample -> gather -> whole update on device) vs the
     oracle's ddpg.py:86-113 sequence on the same sampled rows, 4 steps."""
