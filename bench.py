@@ -14,7 +14,9 @@ ranks / max-over-ranks time.
 Rank 0 prints ONE JSON line with the contract fields plus
   roofline      dominant kernel (HIP-event timed in-process) vs its MFMA peak (fp32:
                 157.3 TF; fp32-on-bf16 gemm_s3: 2.5 PF / 6 products), + frac vs fp32 peak
-  cpu_baseline  the oracle's TF-op-sequence restatement (numpy fp32) on host cores
+  cpu_baseline  torch-CPU restatement of the reference's 8 sess.run calls per step
+                (oracle/torch_cpu.py) on the host cores: 16 threads and 1 thread, + C2
+  step_latency  p10 / median / p90 of per-step wall time (host sync after each step)
   small_batch   the InvertedPendulum B=64 latency-bound configuration (N=1 only)
 """
 import argparse
@@ -144,7 +146,7 @@ def action_selection_latency(actor, S, calls=2000):
     return {"batch": 1, "us_per_call": round(1e6 * el / calls, 2), "calls": calls}
 
 
-def pmc_traffic(cfg_name, kernel):
+def pmc_traffic(cfg_name, kernel, launches_per_step):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/*_pmc_<config>.json, written by profiles/pmc_traffic.py from a
     FETCH_SIZE pass and a WRITE_SIZE pass of this same bench command, with the
@@ -156,55 +158,98 @@ def pmc_traffic(cfg_name, kernel):
             k = json.load(open(fn))["kernels"].get(kernel)
         except (OSError, ValueError):
             continue
-        if k:
-            return round(k["traffic_bytes_per_launch"]), os.path.relpath(fn, ROOT)
+        if not k:
+            continue
+        # the PMC pass must have profiled the same launch set as this run
+        lps = k.get("launches_per_step")
+        if lps is None or abs(lps - launches_per_step) > 1e-6:
+            return None, "%s: launches/step %s != %s (stale pass, not used)" % (
+                os.path.relpath(fn, ROOT), lps, launches_per_step)
+        return round(k["traffic_bytes_per_launch"]), os.path.relpath(fn, ROOT)
     return None, None
 
 
-def cpu_baseline(cfg_name, budget_s=12.0):
-    """Oracle (numpy fp32, TF op sequence incl. actor-forward recompute) on
-    the host cores; a bounded sample of learner steps at the same config."""
-    from oracle import ddpg_oracle as O
+def _cpu_model():
+    cpu, cores = "unknown", os.cpu_count()
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()
-                       if i.get("user_api") == "blas"] or [1])
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = dict(l.split(":", 1) for l in out.splitlines() if ":" in l)
+        cpu = kv.get("Model name", cpu).strip()
+        cores = int(kv["Core(s) per socket"]) * int(kv.get("Socket(s)", "1"))
     except Exception:
-        threads = 1
+        pass
+    return cpu, cores
+
+
+def _cpu_leg(cfg_name, threads, budget_s, max_steps=200):
+    """Time the torch-CPU restatement of the reference's 8-sess.run learner
+    step (oracle/torch_cpu.py) at `threads` intra-op threads, bounded by
+    budget_s seconds or max_steps steps (whichever first, >= 1 step)."""
+    import random
+
+    import torch
+    from oracle.torch_cpu import TorchCPULearner
     S, A, H1, H2, B, scale, _ = CONFIGS[cfg_name]
-    a, c = O.init_params(S, A, H1, H2, seed=1)
-    at, ct = O.init_params(S, A, H1, H2, seed=2)
-    L = O.Learner(S, A, H1, H2, scale, dtype=np.float32,
-                  params={"actor": a, "actor_t": at, "critic": c, "critic_t": ct})
+    torch.set_num_threads(threads)
+    L = TorchCPULearner(S, A, H1, H2, scale, seed=1)
     rng = np.random.default_rng(0)
     pool = 20000
     rows = (rng.standard_normal((pool, S), dtype=np.float32),
             (rng.uniform(-1, 1, (pool, A)) * scale).astype(np.float32),
             rng.standard_normal(pool, dtype=np.float32), rng.random(pool) < 0.01,
             rng.standard_normal((pool, S), dtype=np.float32))
-    import random
-    smp = random.Random(1234)
-    n = 0
-    t0 = time.perf_counter()
+    smp = random.Random(1234)   # replay_buffer.py's random.sample
+    L.step(*(x[np.array(smp.sample(range(pool), B))] for x in rows))  # warm-up
+    n, t0 = 0, time.perf_counter()
     while True:
         idx = np.array(smp.sample(range(pool), B))
         L.step(*(x[idx] for x in rows))
         n += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or n >= 200:
+        if el >= budget_s or n >= max_steps:
             break
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": n / el, "unit": "updates/s", "cores": int(threads), "kind": "port",
-            "sample": "%d learner steps of %s (numpy fp32 oracle, TF op order incl. actor "
-                      "forward recompute; sampler = CPython random.sample) in %.1fs on %s"
-                      % (n, cfg_name.upper(), el, cpu)}
+    return {"value": round(n / el, 3), "unit": "updates/s", "threads": threads, "steps": n,
+            "seconds": round(el, 2)}
+
+
+def cpu_baseline(cfg_name, threads):
+    """the reference's TF CPU path cannot run on the GPU box, so
+    the baseline is a torch-CPU eager, op-for-op restatement of its eight
+    sess.run calls per learner step, timed on this host at `threads` threads and
+    at 1 thread, at the bench config and at C2 (B=64)."""
+    import torch
+    cpu, cores = _cpu_model()
+    prev = torch.get_num_threads()
+    main = _cpu_leg(cfg_name, threads, 12.0)
+    one = _cpu_leg(cfg_name, 1, 10.0)
+    c2 = _cpu_leg("c2", threads, 4.0, 2000)
+    c2_one = _cpu_leg("c2", 1, 4.0, 2000)
+    torch.set_num_threads(prev)
+    return {"value": main["value"], "unit": "updates/s", "cores": threads, "kind": "port",
+            "sample": "%d learner steps of %s in %.1fs: torch-CPU fp32 eager restatement of the "
+                      "reference's 8 sess.run calls per step (oracle/torch_cpu.py; TF 1.3 is not "
+                      "installable on the box), %d threads on %s (%d physical cores on the host; "
+                      "the GPU box's CPU share is 16 threads)"
+                      % (main["steps"], cfg_name.upper(), main["seconds"], threads, cpu, cores),
+            "one_thread": one, "c2_b64": c2, "c2_b64_one_thread": c2_one,
+            "cpu_model": cpu, "host_cores": cores,
+            "historical_reference": "about 52 updates/s end to end incl. env + gRPC "
+                                    "(BASELINE.md, 2017 TF CPU; context only)"}
+
+
+def step_latency_percentiles(fl, sess, n):
+    """Per-step wall time with a host sync after every step (latency view; the
+    headline value above keeps the steps pipelined)."""
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fl.step()
+        sess.sync()
+        ts.append(1000.0 * (time.perf_counter() - t0))
+    p10, p50, p90 = np.percentile(ts, [10, 50, 90])
+    return {"n": n, "p10_ms": round(float(p10), 4), "median_ms": round(float(p50), 4),
+            "p90_ms": round(float(p90), 4)}
 
 
 def main():
@@ -242,6 +287,7 @@ def main():
     ms = 1000.0 * el / args.steps
     value = world * args.steps / el   # batch-B updates processed by all ranks per second
 
+    lat = step_latency_percentiles(fl, sess, min(100, max(10, args.steps)))
     rows, _ = kernel_profile(fl, sess, args.profile_steps)
     by_kernel, (dom_name, dom), gpu_ms, gemm_ms, gemm_flops = summarize_profile(
         rows, args.profile_steps)
@@ -257,7 +303,7 @@ def main():
     else:
         peak = PEAK_FP32_MFMA_TFLOPS
     step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
-    traffic, traffic_src = pmc_traffic(cfg, dom_name)
+    traffic, traffic_src = pmc_traffic(cfg, dom_name, dom["launches"] / args.profile_steps)
     roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -282,6 +328,7 @@ def main():
         "step_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
         "gemm_tflops": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else None,
         "gpu_busy_ms_per_step": round(gpu_ms, 4),
+        "step_latency": lat,
         "roofline": roofline,
         "kernels": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
                         "per_step": v["launches"] / args.profile_steps,
@@ -300,7 +347,7 @@ def main():
     out["hbm_GBs"] = hbm
 
     if world == 1 and rank == 0 and not args.no_small and cfg != "c2":
-        s2, rb2, fl2, actor2 = build_learner("c2", local, 0, 1, 100_000)
+        s2, rb2, fl2, actor2 = build_learner("c2", local, 0, 1, REPLAY_ROWS)
         el2 = timed(fl2, s2, 500, 50, 1)
         rows2, wall2 = kernel_profile(fl2, s2, 100)
         busy2 = sum(r["ms"] for r in rows2.values()) / 100
@@ -313,7 +360,7 @@ def main():
             "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
         s2.close()
     if world == 1 and rank == 0 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(cfg)
+        out["cpu_baseline"] = cpu_baseline(cfg, min(16, os.cpu_count() or 1))
     else:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -170,11 +170,13 @@ class TFAdam:
     def __init__(self, shapes, lr, dtype, beta1=0.9, beta2=0.999, eps=1e-8):
         dt = np.dtype(dtype).type
         self.dt = dt
-        self.lr, self.b1, self.b2, self.eps = dt(lr), dt(beta1), dt(beta2), dt(eps)
+        # the graph's constants are float32 (Adam/learning_rate, Adam/beta1, ...
+        # in model-1410.meta); a float64 run widens those float32 values
+        self.lr, self.b1, self.b2, self.eps = (dt(np.float32(x)) for x in (lr, beta1, beta2, eps))
         self.m = {k: np.zeros(s, dtype) for k, s in shapes.items()}
         self.v = {k: np.zeros(s, dtype) for k, s in shapes.items()}
-        self.b1p = dt(beta1)
-        self.b2p = dt(beta2)
+        self.b1p = self.b1
+        self.b2p = self.b2
 
     def alpha(self):
         one = self.dt(1)
@@ -195,17 +197,18 @@ class TFAdam:
 def soft_update(online, target, tau):
     """networks.py:34-37: target.assign(theta*tau + theta'*(1.-tau))."""
     for k in target:
-        dt = target[k].dtype.type
-        target[k] = online[k] * dt(tau) + target[k] * dt(1.0 - tau)
+        dt = target[k].dtype.type  # float32 graph constants Mul_2/y, Mul_3/y
+        target[k] = online[k] * dt(np.float32(tau)) + target[k] * dt(np.float32(1.0 - tau))
 
 
 def td_target(r, t, q2, gamma):
     """ddpg.py:92-100 vectorised: y = r if t else r + gamma*q'.  Computed at
-    q2's precision (the 2017 numpy semantics: fl(fl(r) + fl(gamma*q')))."""
+    q2's precision (the 2017 numpy semantics: fl(fl(r) + fl(gamma*q')), with
+    the Python-float gamma cast to the float32 array's type)."""
     dt = q2.dtype.type
     r = r.astype(q2.dtype).reshape(-1, 1)
     t = t.astype(bool).reshape(-1, 1)
-    return np.where(t, r, r + dt(gamma) * q2)
+    return np.where(t, r, r + dt(np.float32(gamma)) * q2)  # GAMMA * f32 array -> f32 GAMMA
 
 
 # ---------------------------------------------------------------- init

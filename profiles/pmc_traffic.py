@@ -1,6 +1,10 @@
 """Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-  python profiles/pmc_traffic.py <fetch_dir> <write_dir> <config> > profiles/rN_pmc_<config>.json
+  python profiles/pmc_traffic.py <fetch_dir> <write_dir> <config> <steps> > profiles/rN_pmc_<config>.json
+
+<steps> = fused learner steps the profiled command ran (warmup + steps + the
+bench's latency and profile passes); launches_per_step lets bench.py refuse a
+pass whose launch set does not match the run it reports.
 
 Each pass is its own run of the same bench command (FETCH_SIZE takes 3 of the 4
 TCC slots, WRITE_SIZE 2, so they cannot share one pass), e.g.
@@ -34,6 +38,9 @@ def bench_name(rocprof_name):
     a = [x.strip() for x in targs.split(",")]
     lay = {"0": "RK", "1": "KR"}
     a[0], a[1] = lay.get(a[0], a[0]), lay.get(a[1], a[1])
+    if sym == "gemm_s3_kernel" and len(a) == 3:
+        # bench.py labels the one-plane instantiation gemm_bf16_kernel
+        return "%s<%s,%s>" % ("gemm_s3_kernel" if a[2] == "3" else "gemm_bf16_kernel", a[0], a[1])
     return "%s<%s>" % (sym, ",".join(a))
 
 
@@ -45,7 +52,8 @@ def load(path, counter):
     return agg
 
 
-def main(fetch_dir, write_dir, config):
+def main(fetch_dir, write_dir, config, steps):
+    steps = float(steps)
     f, w = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     out = {"config": config, "source": [fetch_dir, write_dir],
            "correction": "fetch_bytes = 2 x FETCH_SIZE (gfx950 half-count of 128-B requests); "
@@ -55,6 +63,7 @@ def main(fetch_dir, write_dir, config):
         fb = sum(f.get(k, [0.0])) / max(1, len(f.get(k, [])))
         wb = sum(w.get(k, [0.0])) / max(1, len(w.get(k, [])))
         out["kernels"][k] = {"launches": len(f.get(k, [])),
+                             "launches_per_step": len(f.get(k, [])) / steps,
                              "fetch_size_raw_per_launch": fb,
                              "fetch_bytes_per_launch": 2.0 * fb,
                              "write_bytes_per_launch": wb,
@@ -64,4 +73,4 @@ def main(fetch_dir, write_dir, config):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

@@ -1,0 +1,121 @@
+"""GPU parity against the reference's own executed TF graph.
+
+The fixture tests/golden/graph_ip1410.npz is a 3-step trajectory of the
+reference's InvertedPendulum graph (model-1410.meta) executed from its own
+checkpoint -- weights, targets, Adam slots at t ~ 1.4e5 steps and beta powers
+(see tests/test_graph_pin.py for how it pins the oracle).  Here the HIP path
+reproduces it twice:
+  * through the 1:1 C-ABI methods in the exact ddpg.py:86-113 call order
+    (predict_target x2, critic.train, predict, action_gradients, actor.train,
+    update_target_network x2), reading back each gradient the library applied;
+  * through the fused step (ddpg_learner_step_indices over a float64 ring
+    holding each step's batch).
+Bars as everywhere: forward outputs 1e-5, gradients / parameters / Adam slots
+1e-4 (max|x-ref| / max|ref| per tensor).
+"""
+import numpy as np
+import pytest
+
+from test_graph_pin import load_fixture_learner, rel
+
+pytestmark = pytest.mark.gpu
+
+FWD_TOL, GRAD_TOL = 1e-5, 1e-4
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ddpg_oracle
+    return ddpg_oracle
+
+
+def _session(O):
+    import torch
+    assert torch.cuda.is_available()
+    import distributed_ddpg_amd.networks as nets
+    from distributed_ddpg_amd import _lib
+    _, p, z = load_fixture_learner(O)
+    nets.reset_default_graph()
+    actor = nets.ActorNetwork(4, 1, 3.0, 1e-4, 1e-3, None)
+    critic = nets.CriticNetwork(4, 1, 1e-3, 1e-3, actor.get_num_trainable_vars(), None)
+    sess = nets.Session(batch_max=64)
+    actor.set_session(sess)
+    critic.set_session(sess)
+    sess.set_params(_lib.ACTOR, [p["actor"][k] for k in O.ACTOR_KEYS])
+    sess.set_params(_lib.ACTOR_TARGET, [p["actor_t"][k] for k in O.ACTOR_KEYS])
+    sess.set_params(_lib.CRITIC, [p["critic"][k] for k in O.CRITIC_KEYS])
+    sess.set_params(_lib.CRITIC_TARGET, [p["critic_t"][k] for k in O.CRITIC_KEYS])
+    for which, names in ((_lib.ACTOR_ADAM_M, [n + "/Adam" for n in O.CKPT_ACTOR]),
+                         (_lib.ACTOR_ADAM_V, [n + "/Adam_1" for n in O.CKPT_ACTOR]),
+                         (_lib.CRITIC_ADAM_M, [n + "/Adam" for n in O.CKPT_CRITIC]),
+                         (_lib.CRITIC_ADAM_V, [n + "/Adam_1" for n in O.CKPT_CRITIC])):
+        sess.set_params(which, [z["init/" + n] for n in names])
+    sess.set_adam_powers(0, float(z["init/beta1_power"]), float(z["init/beta2_power"]))
+    sess.set_adam_powers(1, float(z["init/beta1_power_1"]), float(z["init/beta2_power_1"]))
+    return sess, actor, critic, z
+
+
+def _check_final(O, sess, z):
+    from distributed_ddpg_amd import _lib
+    for which, names in ((_lib.ACTOR, O.CKPT_ACTOR), (_lib.ACTOR_TARGET, O.CKPT_ACTOR_T),
+                         (_lib.CRITIC, O.CKPT_CRITIC), (_lib.CRITIC_TARGET, O.CKPT_CRITIC_T),
+                         (_lib.ACTOR_ADAM_M, [n + "/Adam" for n in O.CKPT_ACTOR]),
+                         (_lib.ACTOR_ADAM_V, [n + "/Adam_1" for n in O.CKPT_ACTOR]),
+                         (_lib.CRITIC_ADAM_M, [n + "/Adam" for n in O.CKPT_CRITIC]),
+                         (_lib.CRITIC_ADAM_V, [n + "/Adam_1" for n in O.CKPT_CRITIC])):
+        for n, v in zip(names, sess.get_params(which)):
+            assert rel(v, z["final/" + n]) < GRAD_TOL, n
+    for net, sfx in ((0, ""), (1, "_1")):
+        b1p, b2p = sess.get_adam_powers(net)
+        assert b1p == pytest.approx(float(z["final/beta1_power" + sfx]), rel=1e-6)
+        assert b2p == pytest.approx(float(z["final/beta2_power" + sfx]), rel=1e-6)
+
+
+def test_one_to_one_methods_follow_reference_graph(O):
+    from distributed_ddpg_amd import _lib
+    sess, actor, critic, z = _session(O)
+    for step in range(3):
+        p = "step%d/" % step
+        s, a, r, t, s2 = (z[p + k] for k in ("s", "a", "r", "t", "s2"))
+        target_q = critic.predict_target(s2, actor.predict_target(s2))          # ddpg.py:90
+        assert rel(target_q, z[p + "target_q"]) < FWD_TOL, step
+        y = np.where(t[:, None], r[:, None], r[:, None] + 0.99 * target_q)     # ddpg.py:92-97
+        q, _, loss = critic.train(s, a, np.reshape(y, (64, 1)))                 # ddpg.py:100
+        assert rel(q, z[p + "q"]) < FWD_TOL, step
+        assert abs(float(loss) - float(z[p + "loss"])) <= GRAD_TOL * float(z[p + "loss"])
+        for n, g in zip(O.CKPT_CRITIC, sess.get_params(_lib.CRITIC_GRAD)):
+            assert rel(g, z[p + "grad/" + n]) < GRAD_TOL, (step, n)
+        a_outs = actor.predict(s)                                               # ddpg.py:106
+        assert rel(a_outs, z[p + "a_outs"]) < FWD_TOL, step
+        grads = critic.action_gradients(s, a_outs)                              # ddpg.py:107
+        assert rel(grads[0], z[p + "da"]) < GRAD_TOL, step
+        actor.train(s, grads[0])                                                # ddpg.py:109
+        for n, g in zip(O.CKPT_ACTOR, sess.get_params(_lib.ACTOR_GRAD)):
+            assert rel(g, z[p + "grad/" + n]) < GRAD_TOL, (step, n)
+        actor.update_target_network()                                           # ddpg.py:112
+        critic.update_target_network()                                          # ddpg.py:113
+    _check_final(O, sess, z)
+    sess.close()
+
+
+def test_fused_step_follows_reference_graph(O):
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    sess, actor, critic, z = _session(O)
+    rb = ReplayBuffer(3 * 64, 1234)
+    for step in range(3):
+        p = "step%d/" % step
+        rb.add_batch(z[p + "s"], z[p + "a"], z[p + "r"], z[p + "t"], z[p + "s2"])
+    assert rb.f64
+    fl = FusedLearner(sess, rb, 64)
+    for step in range(3):
+        p = "step%d/" % step
+        q_max, loss = fl.step_indices(np.arange(64 * step, 64 * (step + 1)), stats=True)
+        assert abs(loss - float(z[p + "loss"])) <= GRAD_TOL * float(z[p + "loss"])
+        assert q_max == pytest.approx(float(np.max(z[p + "q"])), rel=FWD_TOL)
+        for which, names in ((_lib.CRITIC_GRAD, O.CKPT_CRITIC), (_lib.ACTOR_GRAD, O.CKPT_ACTOR)):
+            for n, g in zip(names, sess.get_params(which)):
+                assert rel(g, z[p + "grad/" + n]) < GRAD_TOL, (step, n)
+    _check_final(O, sess, z)
+    sess.close()
