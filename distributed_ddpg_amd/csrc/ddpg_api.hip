@@ -1207,7 +1207,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     const size_t B = (size_t)c->Bmax;
     const int NTP = std::max(ceil_div(c->AH2, 64), ceil_div(c->CH1, 64));
     const int NTQ = ceil_div(c->CH2, 64);
-    const int mt = ceil_div(c->Bmax, 64);
+    const int mt = ceil_div(c->Bmax, std::min(64, TK_ROWS));  // row blocks of colsum partials
     const int nchunk = ceil_div(c->Bmax, kHeadRows);
     if (const char* mb = getenv("DDPG_GEMM_MIN_BLOCKS")) g_min_blocks = std::max(1, atoi(mb));
     if (const char* xv = getenv("DDPG_XCD")) g_xcd_remap = atoi(xv) != 0;

@@ -54,11 +54,18 @@ struct TkArgs {
 typedef float tk_f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) tk_f32x2 tk_lds_v2;
 
+
+constexpr int TK_VLD = TK_COLS + 4;  // LDS row stride of the output tile (floats)
+constexpr int TK_SMEM =
+    TK_MAXK * TK_COLS > TK_ROWS * TK_VLD ? TK_MAXK * TK_COLS : TK_ROWS * TK_VLD;
+
 __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   // W panel as [k][wave column half][col 0..31][tile 0..1]: one ds_read_b64
-  // per MFMA step gives a lane both of its B operands
-  __shared__ __attribute__((aligned(16))) float Ws[TK_MAXK * TK_COLS];
-  __shared__ float red[2 * TK_COLS];
+  // per MFMA step gives a lane both of its B operands; after the MFMAs the
+  // same LDS holds the raw output tile [64 rows][TK_VLD]
+  __shared__ __attribute__((aligned(16))) float Ws[TK_SMEM];
+  __shared__ float red[8 * TK_COLS];
+  __shared__ __attribute__((aligned(16))) float Xs[TK_ROWS * (TK_MAXK + 4)];
   const TkPart P = blockIdx.z ? args.p[1] : args.p[0];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, h = lane >> 5;
@@ -87,13 +94,16 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
         wv[j] = *reinterpret_cast<const f32x4*>(P.W + (size_t)n * P.ldw + 4 * k4);
     }
   }
-  {
-    const int m = m0 + 32 * wr + li;
-    const float* xr = P.X + (size_t)m * P.ldx + h * KH;
+  // X tile [64 rows][K] -> LDS with coalesced float4 loads (a lane's own row
+  // would otherwise be 8 loads touching 64 different rows per instruction)
+  const int XLD = K + 4;  // padded row stride: conflict-free ds_read_b128 below
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      xv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (q < K8 && m < M) xv[q] = *reinterpret_cast<const f32x4*>(xr + 4 * q);
+  for (int j = 0; j < 4; ++j) {
+    const int f = tid + TK_NT * j, r = f / K4, k4 = f - r * K4, m = m0 + r;
+    if (r < TK_ROWS) {
+      f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < M) x = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + 4 * k4);
+      *reinterpret_cast<f32x4*>(Xs + r * XLD + 4 * k4) = x;
     }
   }
   // ---- W panel -> LDS: column nl -> (half nl >> 6, tile (nl >> 5) & 1, col nl & 31)
@@ -120,6 +130,14 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     }
   }
   __syncthreads();
+  {
+    const float* xr = Xs + (32 * wr + li) * XLD + h * KH;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      xv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (q < K8) xv[q] = *reinterpret_cast<const f32x4*>(xr + 4 * q);
+    }
+  }
   TK_STAMP(1);
   // ---- MFMA: step j contracts k = j (lanes 0-31) and k = KH + j (lanes 32-63)
   f32x16 acc[2];
@@ -140,49 +158,63 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     }
   }
   TK_STAMP(2);
-  // ---- epilogue: lane holds column li of tile t, register r holds row
-  // (r & 3) + 8 (r >> 2) + 4 h
-  const int mb = m0 + 32 * wr + 4 * h;
-  float cs[2];
+  // ---- epilogue.  The raw tile goes through LDS (lane li of tile t holds
+  // column li, register r row (r & 3) + 8 (r >> 2) + 4 h) so that every
+  // element-wise op, the aux loads and the output stores run on float4 rows:
+  // one 16-B access per lane instead of 32 scalar 4-B stores per lane.
+  __syncthreads();  // all waves done reading the W panel
+  {
+    const int rb = 32 * wr + 4 * h;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n = n0 + 64 * wc + 32 * t + li;
-    const bool nok = n < P.N;
-    const float bn = (nok && P.bias) ? P.bias[n] : 0.f;
-    float av[16];
-    if (P.aux) {
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb + (r & 3) + 8 * (r >> 2);
-        av[r] = (nok && m < M) ? P.aux[(size_t)m * P.ldaux + n] : 0.f;
-      }
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = mb + (r & 3) + 8 * (r >> 2);
-      float v = acc[t][r];
-      if (nok && m < M) {
-        if (P.bias) v = __fadd_rn(v, bn);
-        if (P.act == 1) v = elu_f(v);
-        if (P.aux) v = __fmul_rn(v, elu_grad_factor(av[r]));
-        if (P.out) P.out[(size_t)m * P.ldo + n] = v;
-        sum += v;
-      }
-    }
-    cs[t] = sum;
+      for (int r = 0; r < 16; ++r)
+        Ws[(rb + (r & 3) + 8 * (r >> 2)) * TK_VLD + 64 * wc + 32 * t + li] = acc[t][r];
   }
+  __syncthreads();
   TK_STAMP(3);
+  // thread -> column quad c4 = tid & 31, rows rg, rg + 8, ... (rg = tid >> 5)
+  const int c4 = tid & 31, rg = tid >> 5, n = n0 + 4 * c4;
+  const bool nok = n < P.N;  // N % 4 == 0: a quad is all in or all out
+  f32x4 bq = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (P.bias && nok) bq = *reinterpret_cast<const f32x4*>(P.bias + n);
+  f32x4 csum = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int RPT = TK_ROWS / 8;  // rows per thread
+  f32x4 aq[RPT];
+  if (P.aux) {  // all aux loads in flight before the first use
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int m = m0 + rg + 8 * i;
+      aq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (nok && m < M) aq[i] = *reinterpret_cast<const f32x4*>(P.aux + (size_t)m * P.ldaux + n);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int rl = rg + 8 * i, m = m0 + rl;
+    if (!nok || m >= M) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 4 * c4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (P.bias) x = __fadd_rn(x, bq[e]);
+      if (P.act == 1) x = elu_f(x);
+      if (P.aux) x = __fmul_rn(x, elu_grad_factor(aq[i][e]));
+      v[e] = x;
+      csum[e] += x;
+    }
+    if (P.out) *reinterpret_cast<f32x4*>(P.out + (size_t)m * P.ldo + n) = v;
+  }
   if (P.colsum) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) cs[t] += __shfl_xor(cs[t], 32);
-    if (h == 0) {
-      red[wr * TK_COLS + 64 * wc + li] = cs[0];
-      red[wr * TK_COLS + 64 * wc + 32 + li] = cs[1];
-    }
+    for (int e = 0; e < 4; ++e) red[rg * TK_COLS + 4 * c4 + e] = csum[e];
     __syncthreads();
-    if (tid < TK_COLS && n0 + tid < P.N)
-      P.colsum[(size_t)blockIdx.y * P.ld_colsum + n0 + tid] = red[tid] + red[TK_COLS + tid];
+    if (tid < TK_COLS && n0 + tid < P.N) {
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s += red[g * TK_COLS + tid];
+      P.colsum[(size_t)blockIdx.y * P.ld_colsum + n0 + tid] = s;
+    }
   }
 }
 

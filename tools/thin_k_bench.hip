@@ -10,6 +10,9 @@ __device__ unsigned long long g_st[8192 * 5];
     g_st[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 5 + (i)] =      \
         __builtin_amdgcn_s_memtime();
 #include "../distributed_ddpg_amd/csrc/thin_k.h"
+#ifdef WITH_OLD
+#include "../build_variants/thin_k_old.h"
+#endif
 #include <vector>
 #include <algorithm>
 
@@ -34,15 +37,17 @@ static void phases(const char* tag, int nblocks) {
 
 using namespace ddpg;
 
+typedef void (*tk_fn)(TkArgs);
+static tk_fn g_kern = thin_k_kernel;
 static float time_it(const TkArgs& a, int nparts, int reps) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   int nmax = std::max(a.p[0].N, nparts > 1 ? a.p[1].N : 0);
   dim3 grid((nmax + TK_COLS - 1) / TK_COLS, (a.M + TK_ROWS - 1) / TK_ROWS, nparts);
-  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(thin_k_kernel, grid, dim3(TK_NT), 0, 0, a);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(g_kern, grid, dim3(TK_NT), 0, 0, a);
   hipEventRecord(e0);
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(thin_k_kernel, grid, dim3(TK_NT), 0, 0, a);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(g_kern, grid, dim3(TK_NT), 0, 0, a);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -50,7 +55,19 @@ static float time_it(const TkArgs& a, int nparts, int reps) {
   return 1e3f * ms / reps;
 }
 
+static void run_all();
 int main() {
+  printf("== new thin_k_kernel\n");
+  run_all();
+#ifdef WITH_OLD
+  printf("== old thin_k_kernel\n");
+  g_kern = thin_k_old_kernel;
+  run_all();
+#endif
+  return 0;
+}
+
+static void run_all() {
   const int M = 4096, N = 1024;
   float *X, *W, *bias, *out, *aux, *cs;
   hipMalloc(&X, (size_t)M * 64 * 4);
@@ -72,17 +89,17 @@ int main() {
   a.M = M;
   a.p[0] = p;
   printf("K64 bias+elu+store           %.2f us\n", time_it(a, 1, 200));
-  phases("K64", 8 * 64);
+  phases("K64", 8 * 128);
   a.p[0].act = 0;
   printf("K64 bias+store (no elu)      %.2f us\n", time_it(a, 1, 200));
   a.p[0].out = nullptr;
   printf("K64 no store                 %.2f us\n", time_it(a, 1, 200));
-  phases("K64 nostore", 8 * 64);
+  phases("K64 nostore", 8 * 128);
   a.p[0] = p;
   a.p[0].K = 8;
   a.p[0].ldx = 8;
   printf("K8 bias+elu+store            %.2f us\n", time_it(a, 1, 200));
-  phases("K8", 8 * 64);
+  phases("K8", 8 * 128);
   a.p[0] = p;
   a.p[1] = p;
   a.p[1].out = out + N;
@@ -105,5 +122,6 @@ int main() {
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   printf("hipMemset 16 MB              %.2f us\n", 1e3f * ms / 50);
-  return 0;
+  hipFree(X); hipFree(W); hipFree(bias); hipFree(out); hipFree(aux); hipFree(cs);
+  if (hipGetLastError() != hipSuccess) printf("LAUNCH ERROR\n");
 }
