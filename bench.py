@@ -296,9 +296,9 @@ def main():
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_flops = dom["flops"] / dom["launches"]
     achieved = dom_flops / (dom_avg_ms * 1e-3) / 1e12
-    if dom_name.startswith("gemm_bf16"):
+    if dom_name.startswith("gemm_bf16") or (dom_name.startswith("gemm_h") and "NP=1" in dom_name):
         peak = PEAK_BF16_MFMA_TFLOPS
-    elif dom_name.startswith("gemm_s3"):
+    elif dom_name.startswith("gemm_s3") or dom_name.startswith("gemm_h"):
         peak = PEAK_S3_FP32EQ_TFLOPS
     else:
         peak = PEAK_FP32_MFMA_TFLOPS

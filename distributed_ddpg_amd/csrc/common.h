@@ -23,5 +23,53 @@ typedef __attribute__((address_space(1))) float4 glb_f4;
 #define LDS(p) ((lds_f*)(p))
 #define GLB(p) ((glb_f*)(p))
 
+// ---------------------------------------------------------------- bf16 twins
+// bf16 operand types, and the exact three-plane split of an fp32 value used
+// by the bf16 "twins" of fp32 tensors (the operands of gemm_h.h).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+// (x0, x1) -> packed (h, m, l) bf16 pairs: three v_cvt_pk_bf16_f32, the
+// widening of a bf16 pair is two bit operations, the residuals packed f32 subs.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+DDPG_DEV f32x2v widen(bf16x2 b) {
+  const unsigned u = __builtin_bit_cast(unsigned, b);
+  return f32x2v{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xFFFF0000u)};
+}
+DDPG_DEV void split3_pair(f32x2v x, bf16x2& h, bf16x2& m, bf16x2& l) {
+  h = __builtin_convertvector(x, bf16x2);
+  const f32x2v r1 = x - widen(h);  // exact
+  m = __builtin_convertvector(r1, bf16x2);
+  const f32x2v r2 = r1 - widen(m);  // exact
+  l = __builtin_convertvector(r2, bf16x2);
+}
+
+// Store the twin of 4 (or 1) consecutive fp32 values: np = 1 stores bf16(v);
+// np = 3 stores the h / m / l planes, ps elements apart.
+DDPG_DEV void store_twin4(__bf16* q, long long ps, int np, float4 v) {
+  if (np == 3) {
+    bf16x2 h0, m0, l0, h1, m1, l1;
+    split3_pair(f32x2v{v.x, v.y}, h0, m0, l0);
+    split3_pair(f32x2v{v.z, v.w}, h1, m1, l1);
+    *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+    *reinterpret_cast<bf16x4*>(q + ps) = bf16x4{m0[0], m0[1], m1[0], m1[1]};
+    *reinterpret_cast<bf16x4*>(q + 2 * ps) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+  } else {
+    const bf16x2 h0 = __builtin_convertvector(f32x2v{v.x, v.y}, bf16x2);
+    const bf16x2 h1 = __builtin_convertvector(f32x2v{v.z, v.w}, bf16x2);
+    *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+  }
+}
+DDPG_DEV void store_twin1(__bf16* q, long long ps, int np, float x) {
+  const __bf16 h = (__bf16)x;
+  q[0] = h;
+  if (np == 3) {
+    const float r1 = x - (float)h;
+    const __bf16 m = (__bf16)r1;
+    q[ps] = m;
+    q[2 * ps] = (__bf16)(r1 - (float)m);
+  }
+}
+
 // Round-up helper
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

@@ -17,6 +17,7 @@
 #include "gemm_f32.h"
 #include "gemm_bf16.h"
 #include "gemm_s3.h"
+#include "gemm_h.h"
 #include "thin_k.h"
 #include "kernels.h"
 #include "sampler.h"
@@ -178,6 +179,17 @@ struct ddpg_ctx {
   float *ppart, *qpart, *colpart, *headpart;  // partial-sum scratch
   float *ppart_t, *qpart_t;                   // target-path copies (concurrent branch)
   float *slab_W1, *slab_W2, *slab_W3, *slab_Ws, *slab_Wa, *slab_Wh;
+  // bf16 twins (gemm_h.h operands): hnp planes (0 off, 1 bf16 config, 3 the
+  // exact h/m/l split of fp32).  Parameters: theta's twin at wtw, the
+  // target's at wtw + hnp * PT (planes PT apart), current while wtw_ok.
+  // Activations: atw mirrors dact (planes act_n apart); only the buffers in
+  // `twinned` are written (by their producers) and read.
+  int hnp = 0;
+  __bf16* wtw = nullptr;
+  bool wtw_ok = false;
+  __bf16* atw = nullptr;
+  size_t act_n = 0;
+  std::vector<std::pair<const float*, size_t>> twinned;
   int split_cap_W1, split_cap_W2, split_cap_W3, split_cap_Ws, split_cap_Wa, split_cap_Wh;
   int* d_slots = nullptr;
   int* h_slots = nullptr;  // pinned, kSlotRing x Bmax
@@ -225,7 +237,7 @@ struct ddpg_ctx {
 };
 
 static constexpr int kSlotRing = 4;
-static constexpr int kHeadRows = 64;
+static constexpr int kHeadRows = 64, kHeadRows4 = 64;
 
 // ---------------------------------------------------------------- profiling helpers
 static hipEvent_t ev_get(ddpg_ctx* c) {
@@ -343,6 +355,64 @@ static GemmPlan make_plan(int M, int N, int K, int splits, int cap = 64, bool bi
   return p;
 }
 
+// ---------------------------------------------------------------- bf16 twins
+struct Twin {
+  __bf16* p = nullptr;
+  long long ps = 0;  // plane stride (elements)
+};
+
+// Twin of an activation buffer element (nullptr unless the buffer is twinned)
+static Twin act_twin(const ddpg_ctx* c, const float* q) {
+  Twin t;
+  if (!c->hnp || !q) return t;
+  for (const auto& b : c->twinned)
+    if (q >= b.first && q < b.first + b.second) {
+      t.p = c->atw + (q - c->dact);
+      t.ps = (long long)c->act_n;
+      return t;
+    }
+  return t;
+}
+
+// Twin of a GEMM operand: a parameter (theta / target, while the parameter
+// twins are current) or a twinned activation buffer
+static Twin operand_twin(const ddpg_ctx* c, const float* q) {
+  Twin t;
+  if (!c->hnp || !q) return t;
+  const size_t PT = c->L.total;
+  if (c->wtw_ok) {
+    if (q >= c->theta && q < c->theta + PT) {
+      t.p = c->wtw + (q - c->theta);
+      t.ps = (long long)PT;
+      return t;
+    }
+    if (q >= c->target && q < c->target + PT) {
+      t.p = c->wtw + (size_t)c->hnp * PT + (q - c->target);
+      t.ps = (long long)PT;
+      return t;
+    }
+  }
+  return act_twin(c, q);
+}
+
+// Rebuild the parameter twins after a write that bypassed Adam / the soft
+// update (set_params, checkpoint restore, the small-batch path).  Eager:
+// never inside a captured step (the step's own Adam / soft-update launches
+// keep them current).
+static void twins_refresh(ddpg_ctx* c) {
+  if (!c->hnp || c->wtw_ok) return;
+  const size_t PT = c->L.total;
+  hipLaunchKernelGGL(twin_kernel, dim3(2048), dim3(256), 0, c->stream, c->theta, (long long)PT,
+                     c->wtw, (long long)PT, c->hnp);
+  hipLaunchKernelGGL(twin_kernel, dim3(2048), dim3(256), 0, c->stream, c->target, (long long)PT,
+                     c->wtw + (size_t)c->hnp * PT, (long long)PT, c->hnp);
+  HIP_TRY(hipGetLastError());
+  c->wtw_ok = true;
+}
+
+// env DDPG_GEMM_H=0 keeps every GEMM off the bf16-twin kernel
+static int g_gemm_h = -1;
+
 template <int AL, int BL, int VA, int VB>
 static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const GemmArgs& g) {
   if (p.bm == 128 && p.bn == 128)
@@ -379,6 +449,65 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
     if (!ok) throw einval("gemm %s: unsupported epilogue (bias %d act %d post %d)", name, b, e.act,
                           e.post);
   }
+  // a twinned output gets its bf16 twin written by the epilogue
+  GemmEpi ee = e;
+  if (!ee.outh && ee.out && !ee.out_split_stride) {
+    const Twin to = act_twin(c, ee.out);
+    if (to.p) {
+      ee.outh = to.p;
+      ee.h_plane_stride = to.ps;
+      ee.h_planes = c->hnp;
+    }
+  }
+  // bf16-twin operands (gemm_h.h): both operands twinned, K in whole k-tiles
+  if (g_gemm_h < 0) {
+    const char* v = getenv("DDPG_GEMM_H");
+    g_gemm_h = !(v && atoi(v) == 0);
+  }
+  if (g_gemm_h && c->hnp && M >= 128 && N >= 128 && N % 8 == 0 && lda % 8 == 0 &&
+      ldb % 8 == 0 && (AL == L_RK || M % 8 == 0) && (BL == L_RK || N % 8 == 0)) {
+    const int BKh = c->hnp == 1 ? 64 : 32, BMh = c->hnp == 1 ? 256 : 128;
+    const Twin ta = operand_twin(c, A), tb = operand_twin(c, B);
+    if (K % BKh == 0 && ta.p && tb.p && aligned16(ta.p) && aligned16(tb.p)) {
+      GemmPlan h;
+      h.bm = BMh;
+      h.bn = HG_BN;
+      if (splits != 1) {  // ~one block per CU (144 KB of LDS each)
+        const int tiles = ceil_div(M, BMh) * ceil_div(N, HG_BN);
+        splits = std::max(1, 256 / tiles);
+        splits = std::min(splits, std::max(1, K / (4 * BKh)));
+        splits = std::min(splits, cap);
+      }
+      h.kps = rup(ceil_div(K, std::max(1, splits)), BKh);
+      h.splits = ceil_div(K, h.kps);
+      GemmHArgs a;
+      a.A = ta.p;
+      a.B = tb.p;
+      a.pa = ta.ps;
+      a.pb = tb.ps;
+      a.M = M;
+      a.N = N;
+      a.K = K;
+      a.lda = lda;
+      a.ldb = ldb;
+      a.kps = h.kps;
+      a.xcd = g_xcd_remap;
+      a.e = ee;
+      static const char* lay[2] = {"RK", "KR"};
+      char key[112];
+      snprintf(key, sizeof key, "gemm_h_kernel<%s,%s,NP=%d>|%s", lay[AL], lay[BL], c->hnp, name);
+      ProfScope ps(c, key, 2.0 * M * N * (double)K,
+                   2.0 * c->hnp * ((double)M * K + (double)K * N) +
+                       4.0 * (double)M * N * h.splits);
+      const dim3 grid(h.nt(N), h.mt(M), h.splits);
+      if (c->hnp == 1)
+        hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
+      else
+        hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 3, 128, 32>), grid, dim3(HG_NT), 0, c->cur, a);
+      HIP_TRY(hipGetLastError());
+      return h;
+    }
+  }
   GemmArgs g;
   g.A = A;
   g.B = B;
@@ -389,7 +518,7 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   g.ldb = ldb;
   g.kps = p.kps;
   g.xcd = g_xcd_remap;
-  g.e = e;
+  g.e = ee;
   dim3 grid(p.nt(N), p.mt(M), p.splits);
   // profile key "<kernel symbol>|<phase>": the symbol part matches rocprofv3's kernel names
   static const char* lay[2] = {"RK", "KR"};
@@ -484,6 +613,12 @@ static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int
   double flops = 0, bytes = 0;
   for (int i = 0; i < nparts; ++i) {
     a.p[i] = parts[i];
+    const Twin to = act_twin(c, parts[i].out);
+    if (to.p) {
+      a.p[i].outh = to.p;
+      a.p[i].hps = to.ps;
+      a.p[i].hnp = c->hnp;
+    }
     nmax = std::max(nmax, parts[i].N);
     flops += 2.0 * M * parts[i].N * (double)parts[i].K;
     bytes += 4.0 * ((double)M * parts[i].K + (double)parts[i].K * parts[i].N +
@@ -630,7 +765,7 @@ static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
     bytes += (double)tab.seg[i].count * 4.0 * (tab.seg[i].nslab + 1);
   }
   ProfScope ps(c, name, 0, bytes);
-  const int bx = (int)std::min<long long>(512, std::max<long long>(1, (maxc / 4 + 255) / 256));
+  const int bx = (int)std::min<long long>(1024, std::max<long long>(1, (maxc / 4 + 63) / 64));
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, tab.nseg), dim3(256), 0, c->cur, tab);
   HIP_TRY(hipGetLastError());
 }
@@ -669,9 +804,12 @@ static void adam_launch(ddpg_ctx* c, int net, bool advance) {
   c->sb_shadow_ok = false;
   {
     ProfScope ps(c, "adam", 0, 28.0 * n);
+    // keeps theta's twin current, or leaves it stale if it already was
+    __bf16* tw = (c->hnp && c->wtw_ok) ? c->wtw + b : nullptr;
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
                        c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net, lr,
-                       c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon);
+                       c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon, tw, (long long)c->L.total,
+                       c->hnp);
     HIP_TRY(hipGetLastError());
   }
   if (advance) {
@@ -705,15 +843,27 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
                        c->comm ? nullptr : c->dacc);
     HIP_TRY(hipGetLastError());
   }
-  const int nchunk = ceil_div(B, kHeadRows);
+  // column quads when the widths allow; dh_pre's twin is written here
+  const bool hq = c->CH2 % 4 == 0 && c->ldCH2 % 4 == 0;
+  const int hrows = hq ? kHeadRows4 : kHeadRows;
+  const int nchunk = ceil_div(B, hrows);
   float* part_dWo = c->headpart;
   float* part_dbh = c->headpart + (size_t)nchunk * c->CH2;
   float* part_dbo = part_dbh + (size_t)nchunk * c->CH2;
   {
     ProfScope ps(c, "critic_head_bwd", 0, (double)B * c->CH2 * 8.0);
-    hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->CH2, 256), nchunk), dim3(256), 0,
-                       c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->CH2,
-                       kHeadRows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo);
+    if (hq) {
+      const Twin tw = act_twin(c, c->dhp);
+      hipLaunchKernelGGL(critic_head_bwd4_kernel, dim3(ceil_div(c->CH2 / 4, 64), nchunk),
+                         dim3(256), 0, c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]),
+                         B, c->CH2, hrows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo, tw.p,
+                         tw.ps, c->hnp);
+    } else {
+      if (act_twin(c, c->dhp).p) throw einval("dh_pre twin needs CH2 %% 4 == 0");
+      hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->CH2, 256), nchunk), dim3(256), 0,
+                         c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->CH2,
+                         hrows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo);
+    }
     HIP_TRY(hipGetLastError());
   }
   // dWh = cat^T . dh_pre   (split-K slabs; on aux[0] when par)
@@ -882,8 +1032,10 @@ static void soft_update_dev(ddpg_ctx* c, int mask, int pw_mask) {
   const long long n = (long long)(e - b);
   int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
   ProfScope ps(c, "soft_update", 0, 12.0 * n);
+  __bf16* tw = (c->hnp && c->wtw_ok) ? c->wtw + (size_t)c->hnp * c->L.total + b : nullptr;
   hipLaunchKernelGGL(soft_update_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
-                     c->target + b, n, tau, omt, c->dpw, pw_mask, c->cfg.beta1, c->cfg.beta2);
+                     c->target + b, n, tau, omt, c->dpw, pw_mask, c->cfg.beta1, c->cfg.beta2,
+                     tw, (long long)c->L.total, c->hnp);
   HIP_TRY(hipGetLastError());
 }
 
@@ -1055,6 +1207,7 @@ static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B);
 static void learner_step_any(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   if (c->sb_ok && c->world == 1 && B <= c->sb_max_b) {
     learner_step_small(c, rb, B, inv_b);
+    c->wtw_ok = false;  // theta / target moved without their twins
   } else {
     gather_launch(c, rb, B);
     learner_step_dev(c, B, inv_b);
@@ -1066,6 +1219,12 @@ static void upload_rows(ddpg_ctx* c, float* dst, int ld, const float* src, int B
   if (B <= 0 || cols <= 0) return;
   HIP_TRY(hipMemcpy2DAsync(dst, (size_t)ld * 4, src, (size_t)cols * 4, (size_t)cols * 4, B,
                            hipMemcpyHostToDevice, c->stream));
+  const Twin t = act_twin(c, dst);
+  if (t.p) {  // the twin covers the padded rows (pads are zero in both)
+    hipLaunchKernelGGL(twin_kernel, dim3(std::min(ceil_div(B * ld, 256), 2048)), dim3(256), 0,
+                       c->stream, dst, (long long)B * ld, t.p, t.ps, c->hnp);
+    HIP_TRY(hipGetLastError());
+  }
 }
 static void download_rows(ddpg_ctx* c, float* dst, const float* src, int ld, int B, int cols) {
   if (B <= 0 || cols <= 0) return;
@@ -1113,6 +1272,8 @@ static void ctx_free(ddpg_ctx* c) {
   }
   for (void* p : {(void*)c->sb_save, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T,
                   (void*)c->sb_stamps})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->atw, (void*)c->wtw})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc, (void*)c->dstats_all})
@@ -1208,7 +1369,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     const int NTP = std::max(ceil_div(c->AH2, 64), ceil_div(c->CH1, 64));
     const int NTQ = ceil_div(c->CH2, 64);
     const int mt = ceil_div(c->Bmax, std::min(64, TK_ROWS));  // row blocks of colsum partials
-    const int nchunk = ceil_div(c->Bmax, kHeadRows);
+    const int nchunk = ceil_div(c->Bmax, std::min(kHeadRows, kHeadRows4));
     if (const char* mb = getenv("DDPG_GEMM_MIN_BLOCKS")) g_min_blocks = std::max(1, atoi(mb));
     if (const char* xv = getenv("DDPG_XCD")) g_xcd_remap = atoi(xv) != 0;
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
@@ -1252,6 +1413,31 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     for (auto& r : req) {
       *r.p = c->dact + off;
       off += (r.n + 63) / 64 * 64;
+    }
+    // bf16 twins: the bf16 configuration always; fp32 contexts keep exact
+    // three-plane twins unless env DDPG_GEMM_H=0 / DDPG_GEMM=f32
+    {
+      const char* gh = getenv("DDPG_GEMM_H");
+      const char* gf = getenv("DDPG_GEMM");
+      const bool off_h = (gh && atoi(gh) == 0) || (gf && strcmp(gf, "f32") == 0);
+      c->hnp = k.dtype == DDPG_BF16 ? 1 : (off_h ? 0 : 3);
+    }
+    if (c->hnp) {
+      c->act_n = tot;
+      HIP_TRY(hipMalloc(&c->atw, tot * c->hnp * sizeof(__bf16)));
+      HIP_TRY(hipMemset(c->atw, 0, tot * c->hnp * sizeof(__bf16)));
+      HIP_TRY(hipMalloc(&c->wtw, 2 * PT * c->hnp * sizeof(__bf16)));
+      // the GEMM operands among the activations (gemm_h.h needs rows on
+      // 16-B boundaries: ld % 8 == 0)
+      const struct {
+        float* p;
+        int ld;
+      } tw[] = {{c->s, c->ldS},     {c->h1, c->ldAH1},   {c->th1, c->ldAH1}, {c->cat, c->ldC},
+                {c->tcat, c->ldC},  {c->cat2, c->ldC},   {c->dhp, c->ldCH2}, {c->dhp2, c->ldCH2},
+                {c->dz2, c->ldAH2}, {c->dz1, c->ldAH1},  {c->dcat, c->ldC}};
+      for (const auto& t : tw)  // dh_pre's twin comes from the quad head kernel
+        if (t.ld % 8 == 0 && (t.p != c->dhp || c->CH2 % 4 == 0))
+          c->twinned.push_back({t.p, B * (size_t)t.ld});
     }
     HIP_TRY(hipMalloc(&c->d_slots, B * sizeof(int)));
     HIP_TRY(hipHostMalloc(&c->h_slots, kSlotRing * B * sizeof(int)));
@@ -1470,6 +1656,7 @@ int ddpg_set_params(ddpg_ctx* c, int which, const float* host, size_t n) {
     if (n != tot) throw einval("param set %d expects %zu floats, got %zu", which, tot, n);
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->sb_shadow_ok = false;
+    c->wtw_ok = false;
     size_t o = 0;
     for (int i = 0; i < nt; ++i) {
       HIP_TRY(hipMemcpy(base + ts[i].off, host + o, ts[i].count() * 4, hipMemcpyHostToDevice));
@@ -1538,6 +1725,7 @@ int ddpg_set_scaler(ddpg_ctx* c, const double* mean, const double* scale, int S)
 int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_out) {
   return guard(c, [&] {
     check_b(c, B);
+    twins_refresh(c);
     if (c->sb_ok && B * c->S <= SB_PRED_MAX) {
       // action selection (ddpg.py:68-70): one launch, states in the kernel
       // arguments, result written to pinned host memory
@@ -1565,6 +1753,7 @@ int ddpg_critic_forward(ddpg_ctx* c, int target, const float* s, const float* a,
                         float* q_out) {
   return guard(c, [&] {
     check_b(c, B);
+    twins_refresh(c);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     const float* base = target ? c->target : c->theta;
@@ -1581,6 +1770,7 @@ int ddpg_critic_train(ddpg_ctx* c, const float* s, const float* a, const float* 
                       float* q_pre, float* loss) {
   return guard(c, [&] {
     check_b(c, B);
+    twins_refresh(c);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     upload_rows(c, c->y, 1, y, B, 1);
@@ -1598,6 +1788,7 @@ int ddpg_critic_train(ddpg_ctx* c, const float* s, const float* a, const float* 
 int ddpg_critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int B, float* da) {
   return guard(c, [&] {
     check_b(c, B);
+    twins_refresh(c);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
     upload_rows(c, c->a, c->ldA, a, B, c->A);
     critic_action_grad(c, c->s, c->a, B, c->da, nullptr, nullptr);
@@ -1608,6 +1799,7 @@ int ddpg_critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int B, 
 int ddpg_actor_train(ddpg_ctx* c, const float* s, const float* a_gradient, int B) {
   return guard(c, [&] {
     check_b(c, B);
+    twins_refresh(c);
     upload_rows(c, c->s, c->ldS, s, B, c->S);
     // a_gradient as a single "partial" slab [1][B][A] for the dz3 finaliser
     HIP_TRY(hipMemcpyAsync(c->dain, a_gradient, (size_t)B * c->A * 4, hipMemcpyHostToDevice,
@@ -1624,6 +1816,7 @@ int ddpg_actor_train(ddpg_ctx* c, const float* s, const float* a_gradient, int B
 
 int ddpg_soft_update(ddpg_ctx* c, int mask) {
   return guard(c, [&] {
+    twins_refresh(c);
     soft_update_dev(c, mask, 0);
     HIP_TRY(hipStreamSynchronize(c->stream));
   });
@@ -1953,7 +2146,8 @@ static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
                      c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, rb->rsd, rb->rs2d,
                      rb->rrd, c->S, c->A, c->s,
                      c->s2, c->ldS, c->a, c->ldA, c->r, c->t, c->has_scaler ? c->dmean : nullptr,
-                     c->has_scaler ? c->dscale : nullptr);
+                     c->has_scaler ? c->dscale : nullptr, act_twin(c, c->s).p,
+                     act_twin(c, c->s).ps, c->hnp);
   HIP_TRY(hipGetLastError());
 }
 
@@ -1968,6 +2162,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   const int64_t* mine = idx + (size_t)c->rank * B;  // this rank's slice of the global draw
   const float inv_b = 1.0f / (float)Bg;
   sb_refresh_shadows(c);
+  twins_refresh(c);
   // graphs: single-rank, not profiling (RCCL capture and per-kernel events stay eager)
   if (c->use_graph && c->world == 1 && !c->prof) {
     auto& g = c->gslot[c->gcur];

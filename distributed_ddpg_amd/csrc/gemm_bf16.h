@@ -8,9 +8,6 @@
 
 namespace ddpg {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
 constexpr int H_BM = 128, H_BN = 128;
 constexpr int H_ROW = 40;  // bf16 per LDS row (32 k + 8 pad)
 

@@ -61,6 +61,12 @@ struct GemmEpi {
   int proj_n, proj_sn, proj_sa;
   const float* proj;  // Wp[n][a] = proj[n * proj_sn + a * proj_sa]
   float* proj_out;    // [ntile][M][proj_n]
+  // bf16 twin of out (same element offsets, ld = ldo): h_planes = 1 stores
+  // bf16(v); 3 stores the exact h/m/l split of v, planes h_plane_stride apart.
+  // Read by the bf16-operand GEMM (gemm_h.h).  Needs N, ldo % 4 == 0.
+  __bf16* outh;
+  long long h_plane_stride;
+  int h_planes;
 };
 
 struct GemmArgs {
@@ -99,7 +105,7 @@ DDPG_DEV void xcd_tile(int& bx, int& by, int on) {
 // this instead so that every wave passes the same barriers.  Keep in step
 // with the barriers in gemm_epilogue below.
 DDPG_DEV void gemm_epilogue_barriers(const GemmEpi& e) {
-  if (!e.out && !e.colsum && !e.proj_out) return;
+  if (!e.out && !e.outh && !e.colsum && !e.proj_out) return;
   for (int pass = 0; pass < 2; ++pass) {
     __syncthreads();
     __syncthreads();
@@ -147,6 +153,10 @@ DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& 
   }
 }
 
+DDPG_DEV void store_twin(const GemmEpi& e, size_t i, float4 v) {
+  store_twin4(e.outh + i, e.h_plane_stride, e.h_planes, v);
+}
+
 // ---------------------------------------------------------------- epilogue
 // Accumulator layout (32x32 MFMA, dtype independent on gfx950): lane l holds
 // column l&31 of tile (i, j); register r holds row (r&3) + 8(r>>2) + 4(l>>5).
@@ -187,7 +197,7 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   else  // not used by the learner; the host rejects other combinations
     __builtin_trap();
 
-  if (!outp && !e.colsum && !e.proj_out) return;
+  if (!outp && !e.outh && !e.colsum && !e.proj_out) return;
 
   constexpr int VS_LD = TC::VS_LD;
   float* Vs = smem;                      // [WR][VS_LD]
@@ -221,14 +231,16 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           }
     }
     __syncthreads();
-    if (outp) {
+    if (outp || e.outh) {
       const int c4 = tid % C4, rr0 = tid / C4, n = n0 + 4 * c4;
 #pragma unroll 4
       for (int rr = rr0; rr < WR; rr += RPR) {
         const int m = m0 + pass * WR + rr;
         if (m < M) {
           const float4 v = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 4 * c4);
-          float* o = outp + (size_t)m * e.ldo + n;
+          float* o = outp ? outp + (size_t)m * e.ldo + n : nullptr;
+          if (e.outh && n < N) store_twin(e, (size_t)z * e.out_split_stride + (size_t)m * e.ldo + n, v);
+          if (!outp) continue;
           if (vst) {
             if (n < N) *reinterpret_cast<float4*>(o) = v;
           } else {

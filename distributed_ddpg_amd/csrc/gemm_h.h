@@ -1,0 +1,296 @@
+// GEMM on bf16 operands that are already bf16 in HBM (gfx950,
+// v_mfma_f32_32x32x16_bf16, fp32 accumulation), with the fused epilogues of
+// gemm_common.h.  The operands are the bf16 "twins" the producers write next
+// to their fp32 outputs (GEMM epilogues, gather, Adam, soft update):
+//   NP = 1: bf16(x)                      -- the bf16 configuration (C5)
+//   NP = 3: the exact h/m/l split of x   -- fp32-accurate (six plane products,
+//           x y ~ hh + hm + mh + hl + mm + lh, as gemm_s3.h but split once by
+//           the producer instead of in every GEMM's staging loop)
+// so the staging path moves 2 B per element and does no conversion work.
+//
+// Block tile BM x 128 x BK, 512 threads = 8 waves (2 along M x 4 along N),
+// wave tile (BM/2) x 32 = BM/64 MFMA tiles.  Staging is global_load_lds
+// (16 B per lane, 1 KiB per wave instruction) into a 3-stage LDS ring with a
+// counted vmcnt, so tile t+1's loads stay in flight across the one barrier
+// per k-tile while tile t is consumed.  LDS images (per plane):
+//   RK operand (rows contiguous in k): [rows][BK], 16-B chunk c of row r at
+//     chunk c ^ swz(r) -- every 16-lane ds_read_b128 group of a fragment read
+//     hits 16 distinct bank slots;
+//   KR operand (k-major): [BK][128] sub-images with 256-B rows, chunk c of
+//     k-row r at c ^ ((r & 3) << 2 | (r >> 2) & 3), read as the MFMA operand by
+//     two ds_read_b64_tr_b16 (hardware transpose) per fragment, conflict-free.
+// global_load_lds writes lane-linear LDS, so the swizzle is applied to each
+// lane's SOURCE address.  Rows / columns past M or N are clamped (their
+// outputs are discarded by the epilogue); K must be a multiple of BK per split.
+#pragma once
+#include "gemm_bf16.h"
+
+namespace ddpg {
+
+struct GemmHArgs {
+  const __bf16* A;
+  const __bf16* B;
+  long long pa, pb;  // elements between planes (NP = 3)
+  int M, N, K, lda, ldb;
+  int kps;  // k extent per split (multiple of BK)
+  int xcd;
+  GemmEpi e;
+};
+
+constexpr int HG_NT = 512, HG_BN = 128, HG_STAGES = 3;
+
+template <int BM, int BK, int NP>
+struct HgCfg {
+  static constexpr int A_BYTES = BM * BK * 2;  // one plane, one stage
+  static constexpr int B_BYTES = HG_BN * BK * 2;
+  static constexpr int STAGE = NP * (A_BYTES + B_BYTES);
+  static constexpr int A_PW = A_BYTES / 1024 / 8;  // 1-KiB pieces per wave per plane
+  static constexpr int B_PW = B_BYTES / 1024 / 8;
+  static constexpr int G = NP * (A_PW + B_PW);  // glds instructions per wave per k-tile
+  static constexpr int EPI_BYTES = TileCfg<BM, HG_BN>::EPI * 4;
+  static constexpr int SMEM_BYTES =
+      HG_STAGES * STAGE > EPI_BYTES ? HG_STAGES * STAGE : EPI_BYTES;
+  static_assert(A_PW >= 1 && B_PW >= 1 && A_PW * 8192 == A_BYTES && B_PW * 8192 == B_BYTES,
+                "tile must split into whole 1-KiB pieces per wave");
+  static_assert(SMEM_BYTES <= 160 * 1024, "LDS");
+};
+
+// RK image: rows of 2*BK bytes; chunk swizzle spreading 16 consecutive rows
+// over the 16 slots of a 256-B bank row
+template <int BK>
+DDPG_DEV int rk_swz(int row) {
+  if constexpr (BK == 64)
+    return (row >> 1) & 7;
+  else
+    return (row >> 2) & 3;
+}
+DDPG_DEV int kr_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// Source address of this lane's 16 B of piece `piece` (1 KiB of the image).
+// R = row extent of the operand (M or N), r0 = the block's first row,
+// BR = image rows (BM or 128).
+template <int L, int BR, int BK>
+DDPG_DEV const __bf16* hg_src(const __bf16* P, int ld, int R, int r0, int kbeg, int piece,
+                              int lane) {
+  const int off = piece * 1024 + 16 * lane;
+  if constexpr (L == L_RK) {
+    constexpr int RB = 2 * BK;
+    const int row = off / RB, pc = (off % RB) >> 4;
+    const int c = pc ^ rk_swz<BK>(row);
+    const int gr = min(r0 + row, R - 1);
+    return P + (size_t)gr * ld + kbeg + 8 * c;
+  } else {
+    constexpr int SUB = BK * 256;  // one [BK][128] sub-image
+    const int sub = off / SUB, o2 = off % SUB;
+    const int row = o2 >> 8, pc = (o2 & 255) >> 4;
+    const int c = pc ^ kr_swz(row);
+    const int col = min(r0 + 128 * sub + 8 * c, R - 8);  // R % 8 == 0
+    return P + (size_t)(kbeg + row) * ld + col;
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char lds_char;
+
+// Fragment reads as inline asm: the builtin ds_read_b64_tr_b16 makes hipcc
+// wait vmcnt(0) before it (it cannot rule out an overlap with the in-flight
+// global_load_lds writes), which would drain the staging pipeline every
+// k-tile; with every fragment read in asm the k-step loop is software
+// pipelined by hand (counted lgkmcnt, hg_wait).
+DDPG_DEV bf16x4 tr_read(const char* p) {
+  bf16x4 r;
+  const unsigned a = (unsigned)(uintptr_t)(lds_char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+DDPG_DEV bf16x8 b128_read(const char* p) {
+  bf16x8 r;
+  const unsigned a = (unsigned)(uintptr_t)(lds_char*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+// MFMA fragment (lane: row/col li of the operand tile starting at image row
+// `rb`, k = 16 ks + 8 h .. +7) from one plane image.
+template <int L, int BK>
+DDPG_DEV bf16x8 hg_frag(const char* img, int rb, int ks, int lane) {
+  const int h = lane >> 5, li = lane & 31;
+  if constexpr (L == L_RK) {
+    const int r = rb + li;
+    const int c = (2 * ks + h) ^ rk_swz<BK>(r);
+    return b128_read(img + r * (2 * BK) + 16 * c);
+  } else {
+    // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses k-row q,
+    // columns 4p..4p+3 of the group's 16 columns; lane i receives column i.
+    const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = rb + 16 * g + 4 * p;
+    const char* sub = img + (col >> 7) * (BK * 256);
+    const int ch = (col & 127) >> 3;
+    const int k0 = 16 * ks + 8 * h + q, k1 = k0 + 4;
+    const char* a0 = sub + k0 * 256 + 16 * (ch ^ kr_swz(k0)) + 8 * (p & 1);
+    const char* a1 = sub + k1 * 256 + 16 * (ch ^ kr_swz(k1)) + 8 * (p & 1);
+    return __builtin_shufflevector(tr_read(a0), tr_read(a1), 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+// lgkmcnt(0) tied to the fragments, so no MFMA reading them is scheduled
+// above the wait
+template <int N, int NP, int TM>
+DDPG_DEV void hg_wait(bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    asm volatile("" : "+v"(bv[p]));
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av[p][i]));
+  }
+}
+
+template <int AL, int BL, int NP, int BM, int BK>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
+  using C = HgCfg<BM, BK, NP>;
+  constexpr int TM = BM / 64;
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM_BYTES / 4];
+  char* const lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int bx, by;
+  xcd_tile(bx, by, g.xcd);
+  const int n0 = bx * HG_BN, m0 = by * BM, z = blockIdx.z;
+  const int kbeg = z * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+
+  f32x16 acc[TM][1];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+
+  const __bf16* sa[C::A_PW];
+  const __bf16* sb[C::B_PW];
+#pragma unroll
+  for (int i = 0; i < C::A_PW; ++i)
+    sa[i] = hg_src<AL, BM, BK>(g.A, g.lda, g.M, m0, kbeg, wave * C::A_PW + i, lane);
+#pragma unroll
+  for (int i = 0; i < C::B_PW; ++i)
+    sb[i] = hg_src<BL, HG_BN, BK>(g.B, g.ldb, g.N, n0, kbeg, wave * C::B_PW + i, lane);
+  const long long stepA = AL == L_RK ? BK : (long long)BK * g.lda;
+  const long long stepB = BL == L_RK ? BK : (long long)BK * g.ldb;
+
+  // issue k-tile t's loads into stage buffer `buf` (G glds per wave)
+  auto stage = [&](int t, int buf) {
+    char* base = lds + buf * C::STAGE;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int i = 0; i < C::A_PW; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(sa[i] + p * g.pa + t * stepA),
+            (lds_void*)(base + p * C::A_BYTES + (wave * C::A_PW + i) * 1024), 16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < C::B_PW; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(sb[i] + p * g.pb + t * stepB),
+            (lds_void*)(base + NP * C::A_BYTES + p * C::B_BYTES + (wave * C::B_PW + i) * 1024),
+            16, 0, 0);
+    }
+  };
+
+  // R fragment reads per k-step; the counted waits below must fit the 4-bit
+  // lgkmcnt.
+  constexpr int RA = AL == L_RK ? 1 : 2, RB = BL == L_RK ? 1 : 2;
+  constexpr int R = NP * (TM * RA + RB);
+  // NP = 3: the five small plane products go to their own accumulators, so
+  // the main (hh) chain takes one rounding per k-step instead of six
+  f32x16 acs[NP == 3 ? TM : 1];
+  if constexpr (NP == 3) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acs[i][r] = 0.f;
+  }
+  auto read = [&](const char* base, int ks, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      bv[p] = hg_frag<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * 32, ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        av[p][i] = hg_frag<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 32 * i, ks, lane);
+    }
+  };
+  auto mfmas = [&](bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (NP == 3) {
+        // small terms, smallest first: lh, mm, hl, mh, hm  (planes 0 = h, 1 = m, 2 = l)
+        f32x16 c = acs[i];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
+        acs[i] = c;
+      }
+      acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
+    }
+  };
+  // k-step fragments are read DEPTH steps ahead of their MFMAs (a ring of
+  // DEPTH + 1 register sets; counted lgkmcnt, LDS reads return in order).
+  constexpr int KS = BK / 16;
+  constexpr int DEPTH = (2 * R <= 15 && KS > 2) ? 2 : (R <= 15 ? 1 : 0);
+  auto compute = [&](int buf) {
+    const char* base = lds + buf * C::STAGE;
+    bf16x8 fa[DEPTH + 1][NP][TM], fb[DEPTH + 1][NP];
+#pragma unroll
+    for (int ks = 0; ks < DEPTH; ++ks) read(base, ks, fa[ks], fb[ks]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      constexpr int NS = DEPTH + 1;
+      if (ks + DEPTH < KS) read(base, ks + DEPTH, fa[(ks + DEPTH) % NS], fb[(ks + DEPTH) % NS]);
+      const int ahead = (ks + DEPTH < KS ? DEPTH : KS - 1 - ks);  // steps issued after ks
+      if (ahead == 2)
+        hg_wait<(2 * R <= 15 ? 2 * R : 0)>(fa[ks % NS], fb[ks % NS]);
+      else if (ahead == 1)
+        hg_wait<(R <= 15 ? R : 0)>(fa[ks % NS], fb[ks % NS]);
+      else
+        hg_wait<0>(fa[ks % NS], fb[ks % NS]);
+      __builtin_amdgcn_s_setprio(1);
+      mfmas(fa[ks % NS], fb[ks % NS]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  // 3-stage ring: at iteration t, tiles t and t+1 are in flight; wait for t
+  // (this wave's loads), barrier (everyone's loads of t landed, everyone's
+  // reads of t-1 done), refill t-1's buffer with t+2, consume t.
+  if (nk > 0) {
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 2 < nk) stage(t + 2, (t + 2) % HG_STAGES);
+      compute(t % HG_STAGES);
+    }
+  }
+  if constexpr (NP == 3) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] += acs[i];
+  }
+  __syncthreads();  // staging buffers are reused by the epilogue
+  GemmArgs ge;
+  ge.M = g.M;
+  ge.N = g.N;
+  ge.e = g.e;
+  gemm_epilogue<BM, HG_BN, 4>(acc, smem, ge, tid, n0, m0, z, bx, by);
+}
+
+}  // namespace ddpg

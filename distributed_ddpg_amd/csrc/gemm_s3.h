@@ -34,26 +34,6 @@ struct S3Cfg {
 
 constexpr int S3_NT = 512;  // 8 waves: 2 along M x 4 along N, wave tile 64 x 32
 
-// (x0, x1) -> packed (h, m, l) bf16 pairs: three v_cvt_pk_bf16_f32, the
-// widening of a bf16 pair is two bit operations, the residuals packed f32 subs.
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-DDPG_DEV f32x2v widen(bf16x2 b) {
-  const unsigned u = __builtin_bit_cast(unsigned, b);
-  return f32x2v{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xFFFF0000u)};
-}
-DDPG_DEV void split3_pair(f32x2v x, bf16x2& h, bf16x2& m, bf16x2& l) {
-#ifdef S3_TIMING_NOSPLIT  // tuning experiment only: wrong results
-  h = m = l = __builtin_convertvector(x, bf16x2);
-  return;
-#endif
-  h = __builtin_convertvector(x, bf16x2);
-  const f32x2v r1 = x - widen(h);  // exact
-  m = __builtin_convertvector(r1, bf16x2);
-  const f32x2v r2 = r1 - widen(m);  // exact
-  l = __builtin_convertvector(r2, bf16x2);
-}
-
 // 128 rows x 32 k of fp32 for S3_NT threads, 8 floats each.
 //   RK (rows contiguous in k): float4 f = i*512 + tid -> row f>>3, k quad f&7.
 //   KR (k-major): thread (k pair kp = tid&15, row quad rq = tid>>4) loads rows

@@ -24,7 +24,8 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
                                    float* __restrict__ s, float* __restrict__ s2, int lds,
                                    float* __restrict__ a, int lda, float* __restrict__ r,
                                    float* __restrict__ t, const double* __restrict__ mean,
-                                   const double* __restrict__ scale) {
+                                   const double* __restrict__ scale, __bf16* __restrict__ sh,
+                                   long long hps, int hnp) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -47,6 +48,7 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
       }
       s[(size_t)b * lds + j] = x;
       s2[(size_t)b * lds + j] = x2;
+      if (sh) store_twin1(sh + (size_t)b * lds + j, hps, hnp, x);
     }
     for (int j = lane; j < A; j += 64) a[(size_t)b * lda + j] = ra[slot * A + j];
     if (lane == 0) {
@@ -201,6 +203,69 @@ __global__ void critic_head_bwd_kernel(const float* __restrict__ h, int ldh,
   }
 }
 
+// The same on column quads (H2, ldh, ld_dh % 4 == 0): a block covers 64
+// column quads x 4 row groups of a chunk (16-B loads / stores, several rows
+// in flight per thread), the groups' partial sums combined in LDS in a fixed
+// order; also writes dh_pre's bf16 twin (dtw, tnp planes tps apart) for the
+// bf16-operand GEMMs that read it.
+__global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
+    const float* __restrict__ h, int ldh, const float* __restrict__ dq,
+    const float* __restrict__ Wo, int B, int H2, int rows_per_chunk, float* __restrict__ dh_pre,
+    int ld_dh, float* __restrict__ part_dWo, float* __restrict__ part_dbh,
+    float* __restrict__ part_dbo, __bf16* __restrict__ dtw, long long tps, int tnp) {
+  __shared__ float4 red[2][3][64];
+  const int cq = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = 4 * (blockIdx.x * 64 + cq);
+  const int chunk = blockIdx.y;
+  const int b0 = chunk * rows_per_chunk;
+  const int b1 = min(B, b0 + rows_per_chunk);
+  float4 sw = make_float4(0.f, 0.f, 0.f, 0.f), sb = sw;
+  if (j < H2) {
+    const float4 w = *reinterpret_cast<const float4*>(Wo + j);
+#pragma unroll 4
+    for (int b = b0 + rg; b < b1; b += 4) {
+      const float4 hv = *reinterpret_cast<const float4*>(h + (size_t)b * ldh + j);
+      const float d = dq[b];
+      float4 dp;
+      dp.x = __fmul_rn(__fmul_rn(d, w.x), elu_grad_factor(hv.x));
+      dp.y = __fmul_rn(__fmul_rn(d, w.y), elu_grad_factor(hv.y));
+      dp.z = __fmul_rn(__fmul_rn(d, w.z), elu_grad_factor(hv.z));
+      dp.w = __fmul_rn(__fmul_rn(d, w.w), elu_grad_factor(hv.w));
+      *reinterpret_cast<float4*>(dh_pre + (size_t)b * ld_dh + j) = dp;
+      if (dtw) store_twin4(dtw + (size_t)b * ld_dh + j, tps, tnp, dp);
+      sw.x = fmaf(hv.x, d, sw.x);
+      sw.y = fmaf(hv.y, d, sw.y);
+      sw.z = fmaf(hv.z, d, sw.z);
+      sw.w = fmaf(hv.w, d, sw.w);
+      sb.x += dp.x;
+      sb.y += dp.y;
+      sb.z += dp.z;
+      sb.w += dp.w;
+    }
+  }
+  if (rg > 0) {
+    red[0][rg - 1][cq] = sw;
+    red[1][rg - 1][cq] = sb;
+  }
+  __syncthreads();
+  if (rg == 0 && j < H2) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      sw = make_float4(sw.x + red[0][q][cq].x, sw.y + red[0][q][cq].y, sw.z + red[0][q][cq].z,
+                       sw.w + red[0][q][cq].w);
+      sb = make_float4(sb.x + red[1][q][cq].x, sb.y + red[1][q][cq].y, sb.z + red[1][q][cq].z,
+                       sb.w + red[1][q][cq].w);
+    }
+    *reinterpret_cast<float4*>(part_dWo + (size_t)chunk * H2 + j) = sw;
+    *reinterpret_cast<float4*>(part_dbh + (size_t)chunk * H2 + j) = sb;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = b0; b < b1; ++b) s += dq[b];
+    part_dbo[chunk] = s;
+  }
+}
+
 // dQ/da finaliser (networks.py:143 action half) + actor grad_ys
 // (networks.py:44): da = sum_t part[t][b][a];
 // dz3 = TanhGrad(o, (-da) * scale) = ((-da)*scale) * (1 - o*o).
@@ -239,30 +304,60 @@ struct ReduceTable {
   int nseg;
 };
 
-__global__ void reduce_slabs_kernel(ReduceTable tab) {
-  const ReduceSeg g = tab.seg[blockIdx.y];
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const long long tid0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g.vec4) {
-    const long long n4 = g.count >> 2;
-    const long long s4 = g.slab_stride >> 2;
-    const float4* src = reinterpret_cast<const float4*>(g.src);
-    float4* dst = reinterpret_cast<float4*>(g.dst);
-    for (long long i = tid0; i < n4; i += stride) {
-      float4 acc = src[i];
-      for (int k = 1; k < g.nslab; ++k) {
-        const float4 x = src[i + k * s4];
-        acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+// Each block reduces EPB = 256 / SG elements (float4 or scalar) of one
+// segment with SG slab groups (SG = 4, 2 or 1 by the slab count): thread
+// group sg sums slabs sg, sg + SG, ... in order, four loads in flight, and the
+// groups are combined in LDS in a fixed order -- deterministic, and segments
+// with few elements and many slabs (bias partials: 64 slabs of 1024) still
+// put 256 threads on every 64 elements.
+template <class T>
+DDPG_DEV T rs_add(T a, T b);
+template <>
+DDPG_DEV float rs_add(float a, float b) { return a + b; }
+template <>
+DDPG_DEV float4 rs_add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <class T>
+DDPG_DEV void reduce_seg(const T* __restrict__ src, T* __restrict__ dst, long long n,
+                         long long ss, int nslab, T* part) {
+  const int SG = nslab >= 4 ? 4 : (nslab >= 2 ? 2 : 1);
+  const int EPB = 256 / SG;
+  const int e = threadIdx.x % EPB, sg = threadIdx.x / EPB;
+  for (long long i0 = (long long)blockIdx.x * EPB; i0 < n; i0 += (long long)gridDim.x * EPB) {
+    const long long i = i0 + e;
+    T acc{};
+    if (i < n && sg < SG) {
+      int k = sg;
+      acc = src[i + k * ss];
+      k += SG;
+      for (; k + 3 * SG < nslab; k += 4 * SG) {
+        const T x0 = src[i + k * ss], x1 = src[i + (k + SG) * ss];
+        const T x2 = src[i + (k + 2 * SG) * ss], x3 = src[i + (k + 3 * SG) * ss];
+        acc = rs_add(rs_add(rs_add(rs_add(acc, x0), x1), x2), x3);
       }
+      for (; k < nslab; k += SG) acc = rs_add(acc, src[i + k * ss]);
+    }
+    if (sg > 0 && sg < SG) part[(sg - 1) * 256 + e] = acc;
+    __syncthreads();
+    if (sg == 0 && i < n) {
+      for (int q = 1; q < SG; ++q) acc = rs_add(acc, part[(q - 1) * 256 + e]);
       dst[i] = acc;
     }
-  } else {
-    for (long long i = tid0; i < g.count; i += stride) {
-      float acc = g.src[i];
-      for (int k = 1; k < g.nslab; ++k) acc += g.src[i + k * g.slab_stride];
-      g.dst[i] = acc;
-    }
+    __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceTable tab) {
+  __shared__ float4 part[3 * 256];
+  const ReduceSeg g = tab.seg[blockIdx.y];
+  if (g.vec4)
+    reduce_seg<float4>(reinterpret_cast<const float4*>(g.src), reinterpret_cast<float4*>(g.dst),
+                       g.count >> 2, g.slab_stride >> 2, g.nslab, part);
+  else
+    reduce_seg<float>(g.src, g.dst, g.count, g.slab_stride, g.nslab,
+                      reinterpret_cast<float*>(part));
 }
 
 // ---------------------------------------------------------------- K6 Adam
@@ -272,10 +367,12 @@ __global__ void reduce_slabs_kernel(ReduceTable tab) {
 //   p -= (m * alpha) / (sqrt(v) + eps)
 // The beta powers live on device (pw = {b1p, b2p}); the last block to finish
 // advances them (b1p *= b1, b2p *= b2), i.e. the AdamOptimizer._finish update.
+// tw (optional): the bf16 twin of p (tnp planes, tps elements apart), kept
+// current for the bf16-operand GEMMs.
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ g, long long n,
                             const float* __restrict__ pw, float lr, float b1, float b2,
-                            float eps) {
+                            float eps, __bf16* __restrict__ tw, long long tps, int tnp) {
   const float b1p = pw[0], b2p = pw[1];
   const float alpha = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.f, b2p))),
                                 __fsub_rn(1.f, b1p));
@@ -301,6 +398,7 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
     reinterpret_cast<float4*>(p)[i] = P;
     reinterpret_cast<float4*>(m)[i] = Mv;
     reinterpret_cast<float4*>(v)[i] = V;
+    if (tw) store_twin4(tw + 4 * i, tps, tnp, P);
   }
   // tail (n % 4)
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
@@ -308,6 +406,7 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
     m[i] = __fadd_rn(m[i], __fmul_rn(__fsub_rn(g[i], m[i]), omb1));
     v[i] = __fadd_rn(v[i], __fmul_rn(__fsub_rn(__fmul_rn(g[i], g[i]), v[i]), omb2));
     p[i] = __fsub_rn(p[i], __fdiv_rn(__fmul_rn(m[i], alpha), __fadd_rn(__fsqrt_rn(v[i]), eps)));
+    if (tw) store_twin1(tw + i, tps, tnp, p[i]);
   }
 }
 
@@ -329,7 +428,8 @@ __global__ void advance_powers_kernel(float* pw, int mask, float b1, float b2) {
 // networks.py:34-37: target.assign(theta * tau + target * (1. - tau)), fp32.
 __global__ void soft_update_kernel(const float* __restrict__ th, float* __restrict__ tt,
                                    long long n, float tau, float omt, float* pw, int pw_mask,
-                                   float b1, float b2) {
+                                   float b1, float b2, __bf16* __restrict__ tw, long long tps,
+                                   int tnp) {
   if (pw_mask && blockIdx.x == 0 && threadIdx.x == 0) advance_powers(pw, pw_mask, b1, b2);
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -341,11 +441,22 @@ __global__ void soft_update_kernel(const float* __restrict__ th, float* __restri
     b.z = __fadd_rn(__fmul_rn(a.z, tau), __fmul_rn(b.z, omt));
     b.w = __fadd_rn(__fmul_rn(a.w, tau), __fmul_rn(b.w, omt));
     reinterpret_cast<float4*>(tt)[i] = b;
+    if (tw) store_twin4(tw + 4 * i, tps, tnp, b);
   }
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const long long i = (n4 << 2) + threadIdx.x;
     tt[i] = __fadd_rn(__fmul_rn(th[i], tau), __fmul_rn(tt[i], omt));
+    if (tw) store_twin1(tw + i, tps, tnp, tt[i]);
   }
+}
+
+// dst = twin of src[0 .. n) (np planes, ps elements apart): parameter twins
+// after a host write, activation twins after an upload.
+__global__ void twin_kernel(const float* __restrict__ src, long long n, __bf16* __restrict__ dst,
+                            long long ps, int np) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    store_twin1(dst + i, ps, np, src[i]);
 }
 
 }  // namespace ddpg

@@ -42,6 +42,9 @@ struct TkPart {
   int ldaux;
   float* out;         // out[m * ldo + n]
   int ldo;
+  __bf16* outh;       // bf16 twin of out (same offsets; hnp planes, hps apart), or null
+  long long hps;
+  int hnp;
   float* colsum;      // [row block][ld_colsum] partial column sums of v, or null
   int ld_colsum;
 };
@@ -204,6 +207,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
       csum[e] += x;
     }
     if (P.out) *reinterpret_cast<f32x4*>(P.out + (size_t)m * P.ldo + n) = v;
+    if (P.outh) store_twin4(P.outh + (size_t)m * P.ldo + n, P.hps, P.hnp, make_float4(v[0], v[1], v[2], v[3]));
   }
   if (P.colsum) {
 #pragma unroll
