@@ -395,6 +395,13 @@ static Twin operand_twin(const ddpg_ctx* c, const float* q) {
   return act_twin(c, q);
 }
 
+// Row buffers whose columns past the logical width are always zero (their
+// writers touch only the first S / A columns): a contraction over them may run
+// K-padded to its kernel's k step, the padded products being exact zeros.
+static bool zero_padded(const ddpg_ctx* c, const float* q) {
+  return q == c->s || q == c->s2 || q == c->a || q == c->ta2 || q == c->mu || q == c->dz3;
+}
+
 // Rebuild the parameter twins after a write that bypassed Adam / the soft
 // update (set_params, checkpoint restore, the small-batch path).  Eager:
 // never inside a captured step (the step's own Adam / soft-update launches
@@ -468,7 +475,13 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       ldb % 8 == 0 && (AL == L_RK || M % 8 == 0) && (BL == L_RK || N % 8 == 0)) {
     const int BKh = c->hnp == 1 ? 64 : 32, BMh = c->hnp == 1 ? 256 : 128;
     const Twin ta = operand_twin(c, A), tb = operand_twin(c, B);
-    if (K % BKh == 0 && ta.p && tb.p && aligned16(ta.p) && aligned16(tb.p)) {
+    // K-padded first layers: A rows zero past K, B = a parameter twin (its
+    // rows past K are the next tensors' finite values, multiplied by zero)
+    int Kh = K;
+    if (K % BKh && AL == L_RK && BL == L_KR && zero_padded(c, A) && rup(K, BKh) <= lda &&
+        tb.p && tb.ps == (long long)c->L.total && splits == 1)
+      Kh = rup(K, BKh);
+    if (Kh % BKh == 0 && ta.p && tb.p && aligned16(ta.p) && aligned16(tb.p)) {
       GemmPlan h;
       h.bm = BMh;
       h.bn = HG_BN;
@@ -478,8 +491,8 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
         splits = std::min(splits, std::max(1, K / (4 * BKh)));
         splits = std::min(splits, cap);
       }
-      h.kps = rup(ceil_div(K, std::max(1, splits)), BKh);
-      h.splits = ceil_div(K, h.kps);
+      h.kps = rup(ceil_div(Kh, std::max(1, splits)), BKh);
+      h.splits = ceil_div(Kh, h.kps);
       GemmHArgs a;
       a.A = ta.p;
       a.B = tb.p;
@@ -487,7 +500,7 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       a.pb = tb.ps;
       a.M = M;
       a.N = N;
-      a.K = K;
+      a.K = Kh;
       a.lda = lda;
       a.ldb = ldb;
       a.kps = h.kps;
@@ -572,8 +585,10 @@ static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec) {
 // through the GEMMs).  env DDPG_THINK=0 routes every such layer to the GEMMs.
 static int g_thin_k = -1;
 static bool tk_valid(const TkPart& q) {
-  return q.K >= TK_KALIGN && q.K % TK_KALIGN == 0 && q.K <= TK_MAXK && q.ldx % 4 == 0 && q.ldw % 4 == 0 &&
-         q.N % 4 == 0 && q.ldo % 4 == 0 && aligned16(q.X) && aligned16(q.W) &&
+  // W[n][k] (w_nk) may have any stride: the kernel loads it as scalars then
+  return q.K >= TK_KALIGN && q.K % TK_KALIGN == 0 && q.K <= TK_MAXK && q.ldx % 4 == 0 &&
+         (q.w_nk || (q.ldw % 4 == 0 && aligned16(q.W))) && q.N % 4 == 0 && q.ldo % 4 == 0 &&
+         aligned16(q.X) &&
          (!q.out || aligned16(q.out)) && (!q.bias || aligned16(q.bias)) &&
          (!q.aux || (q.ldaux % 4 == 0 && aligned16(q.aux)));
 }
@@ -604,9 +619,18 @@ static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int
     const char* v = getenv("DDPG_THINK");
     g_thin_k = !(v && atoi(v) == 0);
   }
-  if (!g_thin_k || c->cfg.dtype != DDPG_FP32) return 0;
-  for (int i = 0; i < nparts; ++i)
-    if (!tk_valid(parts[i])) return 0;
+  if (!g_thin_k) return 0;
+  TkPart pp[2];
+  for (int i = 0; i < nparts; ++i) {
+    pp[i] = parts[i];
+    // K-padded to the 8-step of the kernel over zero-padded rows (the W rows
+    // past K read are finite parameters of the next tensor, times zero)
+    if (pp[i].K % TK_KALIGN && zero_padded(c, pp[i].X) && rup(pp[i].K, TK_KALIGN) <= pp[i].ldx &&
+        pp[i].W >= c->dparams && pp[i].W < c->dparams + 2 * c->L.total)
+      pp[i].K = rup(pp[i].K, TK_KALIGN);
+    if (!tk_valid(pp[i])) return 0;
+  }
+  parts = pp;
   TkArgs a;
   memset(&a, 0, sizeof a);
   int nmax = 0;
@@ -686,17 +710,21 @@ static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const floa
                                 P(c, base, L.c[CBS]), 1, cat, c->ldC),
                         tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1,
                                 P(c, base, L.c[CBA]), 1, cat + c->CH1, c->ldC)};
-  if (!thin_k_launch(c, "fwd", tp, 2, B)) {
-    e.out = cat;
+  if (!thin_k_launch(c, "fwd", tp, 2, B)) {  // each branch on its own
     e.ldo = c->ldC;
-    e.bias = P(c, base, L.c[CBS]);
     e.act = 1;
-    gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1, c->S,
-                            e);
-    e.out = cat + c->CH1;
-    e.bias = P(c, base, L.c[CBA]);
-    gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1, c->A,
-                            e);
+    if (!thin_k_launch(c, "fwd", &tp[0], 1, B)) {
+      e.out = cat;
+      e.bias = P(c, base, L.c[CBS]);
+      gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1,
+                              c->S, e);
+    }
+    if (!thin_k_launch(c, "fwd", &tp[1], 1, B)) {
+      e.out = cat + c->CH1;
+      e.bias = P(c, base, L.c[CBA]);
+      gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1,
+                              c->A, e);
+    }
   }
   e = epi_none();
   e.bias = P(c, base, L.c[CBH]);
@@ -1334,8 +1362,19 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     c->Bmax = k.batch_max;
     c->world = std::max(1, k.world);
     c->rank = k.rank;
-    c->ldS = rup(c->S, 4);
-    c->ldA = rup(c->A, 4);
+    // bf16 twins: the bf16 configuration always; fp32 contexts keep exact
+    // three-plane twins unless env DDPG_GEMM_H=0 / DDPG_GEMM=f32
+    {
+      const char* gh = getenv("DDPG_GEMM_H");
+      const char* gf = getenv("DDPG_GEMM");
+      const bool off_h = (gh && atoi(gh) == 0) || (gf && strcmp(gf, "f32") == 0);
+      c->hnp = k.dtype == DDPG_BF16 ? 1 : (off_h ? 0 : 3);
+    }
+    // bf16 configuration: state / action rows padded with zeros to whole
+    // k-tiles (64) / thin-K steps (8), so the first layers run K-padded
+    // (K = S = 376 on gemm_h, K = A = 17 on thin_k)
+    c->ldS = c->hnp == 1 ? rup(c->S, 64) : rup(c->S, 4);
+    c->ldA = c->hnp == 1 ? rup(c->A, 8) : rup(c->A, 4);
     c->ldAH1 = rup(c->AH1, 4);
     c->ldAH2 = rup(c->AH2, 4);
     c->ldCH2 = rup(c->CH2, 4);
@@ -1414,14 +1453,6 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       *r.p = c->dact + off;
       off += (r.n + 63) / 64 * 64;
     }
-    // bf16 twins: the bf16 configuration always; fp32 contexts keep exact
-    // three-plane twins unless env DDPG_GEMM_H=0 / DDPG_GEMM=f32
-    {
-      const char* gh = getenv("DDPG_GEMM_H");
-      const char* gf = getenv("DDPG_GEMM");
-      const bool off_h = (gh && atoi(gh) == 0) || (gf && strcmp(gf, "f32") == 0);
-      c->hnp = k.dtype == DDPG_BF16 ? 1 : (off_h ? 0 : 3);
-    }
     if (c->hnp) {
       c->act_n = tot;
       HIP_TRY(hipMalloc(&c->atw, tot * c->hnp * sizeof(__bf16)));
@@ -1432,7 +1463,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       const struct {
         float* p;
         int ld;
-      } tw[] = {{c->s, c->ldS},     {c->h1, c->ldAH1},   {c->th1, c->ldAH1}, {c->cat, c->ldC},
+      } tw[] = {{c->s, c->ldS},     {c->s2, c->ldS},     {c->h1, c->ldAH1},   {c->th1, c->ldAH1}, {c->cat, c->ldC},
                 {c->tcat, c->ldC},  {c->cat2, c->ldC},   {c->dhp, c->ldCH2}, {c->dhp2, c->ldCH2},
                 {c->dz2, c->ldAH2}, {c->dz1, c->ldAH1},  {c->dcat, c->ldC}};
       for (const auto& t : tw)  // dh_pre's twin comes from the quad head kernel
@@ -2147,7 +2178,7 @@ static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
                      rb->rrd, c->S, c->A, c->s,
                      c->s2, c->ldS, c->a, c->ldA, c->r, c->t, c->has_scaler ? c->dmean : nullptr,
                      c->has_scaler ? c->dscale : nullptr, act_twin(c, c->s).p,
-                     act_twin(c, c->s).ps, c->hnp);
+                     act_twin(c, c->s2).p, act_twin(c, c->s).ps, c->hnp);
   HIP_TRY(hipGetLastError());
 }
 

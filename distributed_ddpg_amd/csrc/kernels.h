@@ -25,7 +25,7 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
                                    float* __restrict__ a, int lda, float* __restrict__ r,
                                    float* __restrict__ t, const double* __restrict__ mean,
                                    const double* __restrict__ scale, __bf16* __restrict__ sh,
-                                   long long hps, int hnp) {
+                                   __bf16* __restrict__ s2h, long long hps, int hnp) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -49,6 +49,7 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
       s[(size_t)b * lds + j] = x;
       s2[(size_t)b * lds + j] = x2;
       if (sh) store_twin1(sh + (size_t)b * lds + j, hps, hnp, x);
+      if (s2h) store_twin1(s2h + (size_t)b * lds + j, hps, hnp, x2);
     }
     for (int j = lane; j < A; j += 64) a[(size_t)b * lda + j] = ra[slot * A + j];
     if (lane == 0) {

@@ -87,14 +87,18 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
       wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < K && n < P.N) wv[j] = *reinterpret_cast<const f32x4*>(P.W + (size_t)k * P.ldw + n);
     }
-  } else {  // W[n][k]: float4 of 4 k, column c = tid & 127, k quads (tid >> 7) + 2 j
+  } else {  // W[n][k]: 4 k per load, column c = tid & 127, k quads (tid >> 7) + 2 j
+    // (rows of an unaligned stride, e.g. W3 [H2][A = 17], load as scalars)
     const int c = tid & 127, kq = tid >> 7, n = n0 + c;
+    const bool wvec = ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k4 = kq + 2 * j;
       wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (k4 < K4 && n < P.N)
-        wv[j] = *reinterpret_cast<const f32x4*>(P.W + (size_t)n * P.ldw + 4 * k4);
+      if (k4 < K4 && n < P.N) {
+        const float* q = P.W + (size_t)n * P.ldw + 4 * k4;
+        wv[j] = wvec ? *reinterpret_cast<const f32x4*>(q) : f32x4{q[0], q[1], q[2], q[3]};
+      }
     }
   }
   // X tile [64 rows][K] -> LDS with coalesced float4 loads (a lane's own row

@@ -198,7 +198,9 @@ int main(int argc, char** argv) {
       {"c3 wgrad <KR,KR>", L_KR, L_KR, 3, 1024, 1024, 4096, 4},
   };
   for (const Case& c : cases) {
-    if (only && !strstr(c.name, only)) continue;
+    char full[96];
+    snprintf(full, sizeof full, "%s M=%d N=%d K=%d", c.name, c.M, c.N, c.K);
+    if (only && !strstr(full, only)) continue;
     if (c.np == 1)
       dispatch<1, 256, 64>(c);
     else
