@@ -18,6 +18,7 @@ Rank 0 prints ONE JSON line with the contract fields plus
                 (oracle/torch_cpu.py) on the host cores: 16 threads and 1 thread, + C2
   step_latency  p10 / median / p90 of per-step wall time (host sync after each step)
   small_batch   the InvertedPendulum B=64 latency-bound configuration (N=1 only)
+  c5_bf16       BASELINE configs[4] (S=376, A=17, 2048-wide, B=4096, bf16) (N=1, c3 only)
 """
 import argparse
 import json
@@ -291,7 +292,7 @@ def main():
     rows, _ = kernel_profile(fl, sess, args.profile_steps)
     by_kernel, (dom_name, dom), gpu_ms, gemm_ms, gemm_flops = summarize_profile(
         rows, args.profile_steps)
-    from oracle.ddpg_oracle import flops_per_step
+    from distributed_ddpg_amd.flops import flops_per_step
     step_flops = flops_per_step(S, A, H1, H2, B)
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_flops = dom["flops"] / dom["launches"]
@@ -359,13 +360,43 @@ def main():
             "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1),
             "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
         s2.close()
+    if world == 1 and rank == 0 and not args.no_small and cfg == "c3":
+        # BASELINE configs[4] (C5, bf16) as a secondary line: same step, same
+        # accounting, its own dominant kernel
+        sess.close()
+        s5, rb5, fl5, _ = build_learner("c5", local, 0, 1, args.replay, dtype="bf16")
+        el5 = timed(fl5, s5, 30, 5, 1)
+        rows5, _ = kernel_profile(fl5, s5, 10)
+        bk5, (dn5, d5), gpu5, _, _ = summarize_profile(rows5, 10)
+        S5, A5, H15, H25, B5, _, label5 = CONFIGS["c5"]
+        f5 = flops_per_step(S5, A5, H15, H25, B5)
+        ms5 = 1000.0 * el5 / 30
+        ach5 = (d5["flops"] / d5["launches"]) / (d5["ms"] / d5["launches"] * 1e-3) / 1e12
+        pk5 = PEAK_BF16_MFMA_TFLOPS if ("NP=1" in dn5 or dn5.startswith("gemm_bf16")) \
+            else PEAK_FP32_MFMA_TFLOPS
+        out["c5_bf16"] = {
+            "workload": label5 + ", bf16 GEMM operands (fp32 master weights/accumulation)",
+            "value": round(30 / el5, 3), "unit": "updates/s", "ms_per_step": round(ms5, 4),
+            "dtype": "bf16", "gpu_busy_ms_per_step": round(gpu5, 4),
+            "step_tflops": round(f5 / (ms5 * 1e-3) / 1e12, 2),
+            "mfma_util_step": round(f5 / (ms5 * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "kernel": dn5, "achieved": round(ach5, 2), "peak": pk5,
+                         "unit": "TFLOP/s", "frac": round(ach5 / pk5, 4),
+                         "avg_launch_us": round(1e3 * d5["ms"] / d5["launches"], 2),
+                         "launches_per_step": d5["launches"] / 10},
+            "kernels": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
+                            "per_step": v["launches"] / 10}
+                        for k, v in sorted(bk5.items(), key=lambda kv: -kv[1]["ms"])}}
+        s5.close()
+        sess = None
     if world == 1 and rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(cfg, min(16, os.cpu_count() or 1))
     else:
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    sess.close()
+    if sess is not None:
+        sess.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

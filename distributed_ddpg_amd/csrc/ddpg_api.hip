@@ -177,6 +177,7 @@ struct ddpg_ctx {
   float *th1, *tcat, *ta2, *cat, *h, *dhp, *dcat;
   float *h1, *h2, *o, *mu, *cat2, *dhp2, *da, *dz3, *dz2, *dz1, *dain;
   float *ppart, *qpart, *colpart, *headpart;  // partial-sum scratch
+  float2* lpart = nullptr;                    // loss-kernel block partials
   float *ppart_t, *qpart_t;                   // target-path copies (concurrent branch)
   float *slab_W1, *slab_W2, *slab_W3, *slab_Ws, *slab_Wa, *slab_Wh;
   // bf16 twins (gemm_h.h operands): hnp planes (0 off, 1 bf16 config, 3 the
@@ -435,6 +436,32 @@ static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const Ge
 static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec);
 static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec);
 
+// Whether gemm_launch runs this GEMM on the bf16-twin kernel (both operands
+// twinned, shapes in its tiles, K in whole k-tiles -- or K-padded first
+// layers: A rows zero past K, B a parameter twin whose rows past K are the
+// next tensors' finite values, multiplied by zero); *Kh = the K it runs.
+// Producers use it to skip fp32 copies nobody reads.
+template <int AL, int BL>
+static bool gemm_h_ok(const ddpg_ctx* c, const float* A, int lda, const float* B, int ldb, int M,
+                      int N, int K, int splits, int* Kh) {
+  if (g_gemm_h < 0) {
+    const char* v = getenv("DDPG_GEMM_H");
+    g_gemm_h = !(v && atoi(v) == 0);
+  }
+  if (!(g_gemm_h && c->hnp && M >= 128 && N >= 128 && N % 8 == 0 && lda % 8 == 0 &&
+        ldb % 8 == 0 && (AL == L_RK || M % 8 == 0) && (BL == L_RK || N % 8 == 0)))
+    return false;
+  const int BKh = c->hnp == 1 ? 64 : 32;
+  const Twin ta = operand_twin(c, A), tb = operand_twin(c, B);
+  int k = K;
+  if (K % BKh && AL == L_RK && BL == L_KR && zero_padded(c, A) && rup(K, BKh) <= lda && tb.p &&
+      tb.ps == (long long)c->L.total && splits == 1)
+    k = rup(K, BKh);
+  if (!(k % BKh == 0 && ta.p && tb.p && aligned16(ta.p) && aligned16(tb.p))) return false;
+  *Kh = k;
+  return true;
+}
+
 template <int AL, int BL>
 static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
                             const float* B, int ldb, int M, int N, int K, const GemmEpi& e,
@@ -467,21 +494,11 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
     }
   }
   // bf16-twin operands (gemm_h.h): both operands twinned, K in whole k-tiles
-  if (g_gemm_h < 0) {
-    const char* v = getenv("DDPG_GEMM_H");
-    g_gemm_h = !(v && atoi(v) == 0);
-  }
-  if (g_gemm_h && c->hnp && M >= 128 && N >= 128 && N % 8 == 0 && lda % 8 == 0 &&
-      ldb % 8 == 0 && (AL == L_RK || M % 8 == 0) && (BL == L_RK || N % 8 == 0)) {
+  int Kh = 0;
+  if (gemm_h_ok<AL, BL>(c, A, lda, B, ldb, M, N, K, splits, &Kh)) {
     const int BKh = c->hnp == 1 ? 64 : 32, BMh = c->hnp == 1 ? 256 : 128;
     const Twin ta = operand_twin(c, A), tb = operand_twin(c, B);
-    // K-padded first layers: A rows zero past K, B = a parameter twin (its
-    // rows past K are the next tensors' finite values, multiplied by zero)
-    int Kh = K;
-    if (K % BKh && AL == L_RK && BL == L_KR && zero_padded(c, A) && rup(K, BKh) <= lda &&
-        tb.p && tb.ps == (long long)c->L.total && splits == 1)
-      Kh = rup(K, BKh);
-    if (Kh % BKh == 0 && ta.p && tb.p && aligned16(ta.p) && aligned16(tb.p)) {
+    {
       GemmPlan h;
       h.bm = BMh;
       h.bn = HG_BN;
@@ -638,7 +655,7 @@ static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int
   for (int i = 0; i < nparts; ++i) {
     a.p[i] = parts[i];
     const Twin to = act_twin(c, parts[i].out);
-    if (to.p) {
+    if (to.p && !a.p[i].outh) {
       a.p[i].outh = to.p;
       a.p[i].hps = to.ps;
       a.p[i].hnp = c->hnp;
@@ -668,10 +685,23 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
                       float* h2, float* o, float* mu) {
   const Layout& L = c->L;
   GemmEpi e = epi_none();
-  const TkPart tp = tk_part(s, c->ldS, c->S, P(c, base, L.a[AW1]), c->AH1, 0, c->AH1,
-                            P(c, base, L.a[AB1]), 1, h1, c->ldAH1);
+  // the target path's h1 is read only by the next layer: when that runs on
+  // the twin GEMM, only the twin is written
+  int kh;
+  const Twin h1t = (h1 == c->th1 && gemm_h_ok<L_RK, L_KR>(c, h1, c->ldAH1, P(c, base, L.a[AW2]),
+                                                           c->AH2, B, c->AH2, c->AH1, 1, &kh))
+                       ? act_twin(c, h1)
+                       : Twin();
+  TkPart tp = tk_part(s, c->ldS, c->S, P(c, base, L.a[AW1]), c->AH1, 0, c->AH1,
+                      P(c, base, L.a[AB1]), 1, h1t.p ? nullptr : h1, c->ldAH1);
+  tp.outh = h1t.p;
+  tp.hps = h1t.ps;
+  tp.hnp = c->hnp;
   if (!thin_k_launch(c, "fwd", &tp, 1, B)) {
-    e.out = h1;
+    e.out = h1t.p ? nullptr : h1;
+    e.outh = h1t.p;
+    e.h_plane_stride = h1t.ps;
+    e.h_planes = c->hnp;
     e.ldo = c->ldAH1;
     e.bias = P(c, base, L.a[AB1]);
     e.act = 1;
@@ -705,22 +735,39 @@ static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const floa
                       float* cat, float* h_out, int mode, float* dhp_out) {
   const Layout& L = c->L;
   GemmEpi e = epi_none();
+  // the target path's concat is read only by the hidden layer: when that runs
+  // on the twin GEMM, only the twin is written
+  int kh;
+  const Twin ct = (cat == c->tcat && gemm_h_ok<L_RK, L_KR>(c, cat, c->ldC, P(c, base, L.c[CWH]),
+                                                            c->CH2, B, c->CH2, 2 * c->CH1, 1, &kh))
+                      ? act_twin(c, cat)
+                      : Twin();
   // [state branch | action branch] of the concat in one launch
-  const TkPart tp[2] = {tk_part(s, c->ldS, c->S, P(c, base, L.c[CWS]), c->CH1, 0, c->CH1,
-                                P(c, base, L.c[CBS]), 1, cat, c->ldC),
-                        tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1,
-                                P(c, base, L.c[CBA]), 1, cat + c->CH1, c->ldC)};
+  TkPart tp[2] = {tk_part(s, c->ldS, c->S, P(c, base, L.c[CWS]), c->CH1, 0, c->CH1,
+                          P(c, base, L.c[CBS]), 1, ct.p ? nullptr : cat, c->ldC),
+                  tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1,
+                          P(c, base, L.c[CBA]), 1, ct.p ? nullptr : cat + c->CH1, c->ldC)};
+  if (ct.p)
+    for (int i = 0; i < 2; ++i) {
+      tp[i].outh = ct.p + i * c->CH1;
+      tp[i].hps = ct.ps;
+      tp[i].hnp = c->hnp;
+    }
   if (!thin_k_launch(c, "fwd", tp, 2, B)) {  // each branch on its own
     e.ldo = c->ldC;
     e.act = 1;
+    e.h_plane_stride = ct.ps;
+    e.h_planes = c->hnp;
     if (!thin_k_launch(c, "fwd", &tp[0], 1, B)) {
-      e.out = cat;
+      e.out = ct.p ? nullptr : cat;
+      e.outh = ct.p;
       e.bias = P(c, base, L.c[CBS]);
       gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1,
                               c->S, e);
     }
     if (!thin_k_launch(c, "fwd", &tp[1], 1, B)) {
-      e.out = cat + c->CH1;
+      e.out = ct.p ? nullptr : cat + c->CH1;
+      e.outh = ct.p ? ct.p + c->CH1 : nullptr;
       e.bias = P(c, base, L.c[CBA]);
       gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1,
                               c->A, e);
@@ -734,6 +781,15 @@ static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const floa
     e.pw = P(c, base, L.c[CWO]);
     e.out = dhp_out;
     e.ldo = c->ldCH2;
+    // dh_pre of the action-gradient path feeds only the dx_da GEMM
+    const float* whA = P(c, base, L.c[CWH]) + (size_t)c->CH1 * c->CH2;
+    if (gemm_h_ok<L_RK, L_RK>(c, dhp_out, c->ldCH2, whA, c->CH2, B, c->CH1, c->CH2, 1, &kh)) {
+      const Twin dt = act_twin(c, dhp_out);
+      e.out = nullptr;
+      e.outh = dt.p;
+      e.h_plane_stride = dt.ps;
+      e.h_planes = c->hnp;
+    }
   } else {
     e.out = (mode == 0) ? h_out : nullptr;
     e.ldo = c->ldCH2;
@@ -866,9 +922,9 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   {
     ProfScope ps(c, "critic_loss", 0, 0);
     // world > 1: the per-step stats are reduced over ranks below, then accumulated
-    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, c->cur, c->qpart, nq, B,
-                       P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq, c->dstats,
-                       c->comm ? nullptr : c->dacc);
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->cur,
+                       c->qpart, nq, B, P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq,
+                       c->lpart);
     HIP_TRY(hipGetLastError());
   }
   // column quads when the widths allow; dh_pre's twin is written here
@@ -885,12 +941,14 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
       hipLaunchKernelGGL(critic_head_bwd4_kernel, dim3(ceil_div(c->CH2 / 4, 64), nchunk),
                          dim3(256), 0, c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]),
                          B, c->CH2, hrows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo, tw.p,
-                         tw.ps, c->hnp);
+                         tw.ps, c->hnp, c->lpart, ceil_div(B, 256), inv_b, c->dstats,
+                         c->comm ? nullptr : c->dacc);
     } else {
       if (act_twin(c, c->dhp).p) throw einval("dh_pre twin needs CH2 %% 4 == 0");
       hipLaunchKernelGGL(critic_head_bwd_kernel, dim3(ceil_div(c->CH2, 256), nchunk), dim3(256), 0,
                          c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]), B, c->CH2,
-                         hrows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo);
+                         hrows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo, c->lpart,
+                         ceil_div(B, 256), inv_b, c->dstats, c->comm ? nullptr : c->dacc);
     }
     HIP_TRY(hipGetLastError());
   }
@@ -1437,6 +1495,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
         {&c->qpart_t, (size_t)NTQ * B},
         {&c->colpart, (size_t)mt * std::max(2 * c->CH1, c->AH2 + c->AH1)},
         {&c->headpart, (size_t)nchunk * (2 * c->CH2 + 1)},
+        {reinterpret_cast<float**>(&c->lpart), 2 * (size_t)ceil_div(c->Bmax, 256)},
         {&c->slab_W1, (size_t)c->split_cap_W1 * c->S * c->AH1},
         {&c->slab_W2, (size_t)c->split_cap_W2 * c->AH1 * c->AH2},
         {&c->slab_W3, (size_t)c->split_cap_W3 * c->AH2 * c->A},

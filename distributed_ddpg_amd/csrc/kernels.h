@@ -126,46 +126,58 @@ __global__ void critic_q_kernel(const float* __restrict__ qpart, int NT, int B,
 }
 
 // Critic train head (networks.py:136, tflearn.mean_square): q = sum + bo,
-// L = mean((y - q)^2), dq = -((1/B) * (2 * (y - q))).  Single block; also
-// writes per-step stats {q_max, loss} and accumulates them.
-// inv_b is 1/B_global; the loss written is this rank's share of the mean.
-__global__ void critic_loss_kernel(const float* __restrict__ qpart, int NT, int B,
-                                   const float* __restrict__ bo, const float* __restrict__ y,
-                                   float inv_b, float* __restrict__ q, float* __restrict__ dq,
-                                   float* __restrict__ stats /* [q_max, loss] */,
-                                   double* __restrict__ acc /* [qmax_sum, loss_sum, steps] */) {
-  __shared__ float s_sum[1024];
-  __shared__ float s_max[1024];
+// L = mean((y - q)^2), dq = -((1/B) * (2 * (y - q))).  One row per thread,
+// 256 rows per block; each block leaves its {sum (y-q)^2, max q} partial in
+// lpart, and the critic-head kernel that runs next folds them (stats_fold).
+// inv_b is 1/B_global; the loss is this rank's share of the mean.
+__global__ __launch_bounds__(256) void critic_loss_kernel(
+    const float* __restrict__ qpart, int NT, int B, const float* __restrict__ bo,
+    const float* __restrict__ y, float inv_b, float* __restrict__ q, float* __restrict__ dq,
+    float2* __restrict__ lpart) {
+  __shared__ float s_sum[256];
+  __shared__ float s_max[256];
+  const int b = blockIdx.x * 256 + threadIdx.x;
   float lsum = 0.f, lmax = -INFINITY;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    float z = 0.f;
+  if (b < B) {
+    float z = 0.f;  // slab order; loads issued ahead of the adds
+#pragma unroll 8
     for (int tt = 0; tt < NT; ++tt) z += qpart[(size_t)tt * B + b];
     z = __fadd_rn(z, bo[0]);
     q[b] = z;
     const float d = __fsub_rn(y[b], z);
     dq[b] = -__fmul_rn(inv_b, __fmul_rn(2.f, d));
-    lsum += __fmul_rn(d, d);
-    lmax = fmaxf(lmax, z);
+    lsum = __fmul_rn(d, d);
+    lmax = z;
   }
   s_sum[threadIdx.x] = lsum;
   s_max[threadIdx.x] = lmax;
   __syncthreads();
-  for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+  for (int w = 128; w > 0; w >>= 1) {
     if (threadIdx.x < w) {
       s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
       s_max[threadIdx.x] = fmaxf(s_max[threadIdx.x], s_max[threadIdx.x + w]);
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const float loss = __fmul_rn(s_sum[0], inv_b);
-    stats[0] = s_max[0];
-    stats[1] = loss;
-    if (acc) {
-      acc[0] += (double)s_max[0];
-      acc[1] += (double)loss;
-      acc[2] += 1.0;
-    }
+  if (threadIdx.x == 0) lpart[blockIdx.x] = make_float2(s_sum[0], s_max[0]);
+}
+
+// Per-step stats {q_max, loss} from the loss kernel's block partials (fixed
+// order), and their running sums (acc may be null).  One thread.
+DDPG_DEV void stats_fold(const float2* __restrict__ lpart, int nlp, float inv_b,
+                         float* __restrict__ stats, double* __restrict__ acc) {
+  float sum = 0.f, mx = -INFINITY;
+  for (int i = 0; i < nlp; ++i) {
+    sum += lpart[i].x;
+    mx = fmaxf(mx, lpart[i].y);
+  }
+  const float loss = __fmul_rn(sum, inv_b);
+  stats[0] = mx;
+  stats[1] = loss;
+  if (acc) {
+    acc[0] += (double)mx;
+    acc[1] += (double)loss;
+    acc[2] += 1.0;
   }
 }
 
@@ -178,7 +190,9 @@ __global__ void critic_head_bwd_kernel(const float* __restrict__ h, int ldh,
                                        int rows_per_chunk, float* __restrict__ dh_pre,
                                        int ld_dh, float* __restrict__ part_dWo,
                                        float* __restrict__ part_dbh,
-                                       float* __restrict__ part_dbo) {
+                                       float* __restrict__ part_dbo,
+                                       const float2* __restrict__ lpart, int nlp, float inv_b,
+                                       float* __restrict__ stats, double* __restrict__ acc) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int chunk = blockIdx.y;
   const int b0 = chunk * rows_per_chunk;
@@ -201,6 +215,7 @@ __global__ void critic_head_bwd_kernel(const float* __restrict__ h, int ldh,
     float s = 0.f;
     for (int b = b0; b < b1; ++b) s += dq[b];
     part_dbo[chunk] = s;
+    if (chunk == 0) stats_fold(lpart, nlp, inv_b, stats, acc);
   }
 }
 
@@ -213,7 +228,9 @@ __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
     const float* __restrict__ h, int ldh, const float* __restrict__ dq,
     const float* __restrict__ Wo, int B, int H2, int rows_per_chunk, float* __restrict__ dh_pre,
     int ld_dh, float* __restrict__ part_dWo, float* __restrict__ part_dbh,
-    float* __restrict__ part_dbo, __bf16* __restrict__ dtw, long long tps, int tnp) {
+    float* __restrict__ part_dbo, __bf16* __restrict__ dtw, long long tps, int tnp,
+    const float2* __restrict__ lpart, int nlp, float inv_b, float* __restrict__ stats,
+    double* __restrict__ acc) {
   __shared__ float4 red[2][3][64];
   const int cq = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int j = 4 * (blockIdx.x * 64 + cq);
@@ -264,6 +281,7 @@ __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
     float s = 0.f;
     for (int b = b0; b < b1; ++b) s += dq[b];
     part_dbo[chunk] = s;
+    if (chunk == 0) stats_fold(lpart, nlp, inv_b, stats, acc);
   }
 }
 

@@ -201,3 +201,12 @@ def test_learner_step_fp32_tracks_fp64():
 def test_flops_formula():
     assert O.flops_per_step(64, 16, 1024, 1024, 4096, survey=True) == pytest.approx(142.46e9,
                                                                                      rel=1e-4)
+
+
+def test_bench_flop_accounting_matches_oracle():
+    """bench.py counts FLOP with distributed_ddpg_amd.flops; it must agree with
+    the oracle's count."""
+    from distributed_ddpg_amd.flops import flops_per_step as F
+    for args in [(64, 16, 1024, 1024, 4096), (376, 17, 2048, 2048, 4096), (4, 1, 128, 200, 64)]:
+        for kw in ({}, {"survey": True}, {"tf_recompute": True}):
+            assert F(*args, **kw) == O.flops_per_step(*args, **kw)
