@@ -258,9 +258,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
         hg_wait<(R <= 15 ? R : 0)>(fa[ks % NS], fb[ks % NS]);
       else
         hg_wait<0>(fa[ks % NS], fb[ks % NS]);
-      __builtin_amdgcn_s_setprio(1);
       mfmas(fa[ks % NS], fb[ks % NS]);
-      __builtin_amdgcn_s_setprio(0);
     }
   };
 
