@@ -196,6 +196,10 @@ int main(int argc, char** argv) {
       {"c3 dx <RK,RK>", L_RK, L_RK, 3, 4096, 1024, 1024, 1},
       {"c3 wgrad <KR,KR>", L_KR, L_KR, 3, 2048, 1024, 4096, 2},
       {"c3 wgrad <KR,KR>", L_KR, L_KR, 3, 1024, 1024, 4096, 4},
+      {"c3 thin fwd <RK,KR>", L_RK, L_KR, 3, 4096, 1024, 64, 1},
+      {"c3 thin fwd <RK,KR>", L_RK, L_KR, 3, 4096, 1024, 32, 1},
+      {"c3 thin wgrad <KR,KR>", L_KR, L_KR, 3, 64, 1024, 4096, 16},
+      {"c3 thin wgrad <KR,KR>", L_KR, L_KR, 3, 64, 1024, 4096, 32},
   };
   for (const Case& c : cases) {
     char full[96];
