@@ -300,6 +300,7 @@ static int g_xcd_remap = 1;  // env DDPG_XCD=0 disables
 
 struct GemmPlan {
   int bm = 128, bn = 128, splits = 1, kps = 0;
+  bool direct = false;  // the result went straight to the caller's `direct` buffer
   int mt(int M) const { return ceil_div(M, bm); }
   int nt(int N) const { return ceil_div(N, bn); }
 };
@@ -462,10 +463,12 @@ static bool gemm_h_ok(const ddpg_ctx* c, const float* A, int lda, const float* B
   return true;
 }
 
+// direct: for a split-K weight gradient, where to write the result when the
+// plan ends up with one split (no slab, no reduction; plan.direct = true).
 template <int AL, int BL>
 static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
                             const float* B, int ldb, int M, int N, int K, const GemmEpi& e,
-                            int splits = 1, int cap = 64) {
+                            int splits = 1, int cap = 64, float* direct = nullptr) {
   const int contA = (AL == L_RK) ? K : M;
   const int contB = (BL == L_RK) ? K : N;
   const bool va = (contA % 4 == 0) && (lda % 4 == 0) && aligned16(A);
@@ -510,6 +513,11 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       }
       h.kps = rup(ceil_div(Kh, std::max(1, splits)), BKh);
       h.splits = ceil_div(Kh, h.kps);
+      if (h.splits == 1 && direct) {
+        ee.out = direct;
+        ee.out_split_stride = 0;
+        h.direct = true;
+      }
       GemmHArgs a;
       a.A = ta.p;
       a.B = tb.p;
@@ -537,6 +545,11 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       HIP_TRY(hipGetLastError());
       return h;
     }
+  }
+  if (p.splits == 1 && direct) {
+    ee.out = direct;
+    ee.out_split_stride = 0;
+    p.direct = true;
   }
   GemmArgs g;
   g.A = A;
@@ -841,6 +854,12 @@ static void add_seg(ReduceTable& t, const float* src, float* dst, long long stri
   s.vec4 = (count % 4 == 0) && (stride % 4 == 0) && aligned16(src) && aligned16(dst);
 }
 
+// a weight-gradient GEMM's slabs, unless it wrote the gradient directly
+static void add_wgrad(ReduceTable& t, const GemmPlan& p, const float* slab, float* dst,
+                      long long count) {
+  if (!p.direct) add_seg(t, slab, dst, count, p.splits, count);
+}
+
 static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
   long long maxc = 1;
   double bytes = 0;
@@ -934,13 +953,21 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   float* part_dWo = c->headpart;
   float* part_dbh = c->headpart + (size_t)nchunk * c->CH2;
   float* part_dbo = part_dbh + (size_t)nchunk * c->CH2;
+  // dh_pre feeds dWh and dcat only: when both run on the twin GEMM, only its
+  // twin is written
+  int kh;
+  const bool dhp_twin_only =
+      gemm_h_ok<L_KR, L_KR>(c, c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1, c->CH2, B, 0, &kh) &&
+      gemm_h_ok<L_RK, L_RK>(c, c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]), c->CH2, B,
+                            2 * c->CH1, c->CH2, 1, &kh);
   {
     ProfScope ps(c, "critic_head_bwd", 0, (double)B * c->CH2 * 8.0);
     if (hq) {
       const Twin tw = act_twin(c, c->dhp);
       hipLaunchKernelGGL(critic_head_bwd4_kernel, dim3(ceil_div(c->CH2 / 4, 64), nchunk),
                          dim3(256), 0, c->cur, c->h, c->ldCH2, c->dq, P(c, c->theta, L.c[CWO]),
-                         B, c->CH2, hrows, c->dhp, c->ldCH2, part_dWo, part_dbh, part_dbo, tw.p,
+                         B, c->CH2, hrows, dhp_twin_only ? nullptr : c->dhp, c->ldCH2, part_dWo,
+                         part_dbh, part_dbo, tw.p,
                          tw.ps, c->hnp, c->lpart, ceil_div(B, 256), inv_b, c->dstats,
                          c->comm ? nullptr : c->dacc);
     } else {
@@ -963,7 +990,8 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   e.ldo = c->CH2;
   e.out_split_stride = (long long)2 * c->CH1 * c->CH2;
   GemmPlan pWh = gemm_launch<L_KR, L_KR>(c, "wgrad", c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1,
-                                         c->CH2, B, e, 0, c->split_cap_Wh);
+                                         c->CH2, B, e, 0, c->split_cap_Wh,
+                                         c->grad + L.c[CWH].off);
   c->cur = main;
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
   e = epi_none();
@@ -983,24 +1011,22 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   e.ldo = c->CH1;
   e.out_split_stride = (long long)c->S * c->CH1;
   GemmPlan pWs = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1,
-                                         B, e, 0, c->split_cap_Ws);
+                                         B, e, 0, c->split_cap_Ws, c->grad + L.c[CWS].off);
   e.out = c->slab_Wa;
   e.out_split_stride = (long long)c->A * c->CH1;
   GemmPlan pWa = gemm_launch<L_KR, L_KR>(c, "wgrad", c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A,
-                                         c->CH1, B, e, 0, c->split_cap_Wa);
+                                         c->CH1, B, e, 0, c->split_cap_Wa,
+                                         c->grad + L.c[CWA].off);
   if (par) fork_to(c, 5, c->aux[0], main);  // join dWh
   // gather every critic gradient into the flat grad buffer
   float* G = c->grad;
   ReduceTable tab;
   tab.nseg = 0;
-  add_seg(tab, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1, pWs.splits,
-          (long long)c->S * c->CH1);
+  add_wgrad(tab, pWs, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1);
   add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, c->CH1);
-  add_seg(tab, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1, pWa.splits,
-          (long long)c->A * c->CH1);
+  add_wgrad(tab, pWa, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1);
   add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, c->CH1);
-  add_seg(tab, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->CH1 * c->CH2, pWh.splits,
-          (long long)2 * c->CH1 * c->CH2);
+  add_wgrad(tab, pWh, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->CH1 * c->CH2);
   add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, c->CH2);
   add_seg(tab, part_dWo, G + L.c[CWO].off, c->CH2, nchunk, c->CH2);
   add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1);
@@ -1027,11 +1053,27 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   e.ldo = c->A;
   e.out_split_stride = (long long)c->AH2 * c->A;
   GemmPlan pW3 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A,
-                                         B, e, 0, c->split_cap_W3);
+                                         B, e, 0, c->split_cap_W3, G + L.a[AW3].off);
   c->cur = main;
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
+  // dz2 feeds dW2 and dz1 only; dz1 feeds dW1 only: twin-only when those run
+  // on the twin GEMM
+  int kh;
+  const Twin dz2t =
+      (gemm_h_ok<L_KR, L_KR>(c, c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1, c->AH2, B, 0, &kh) &&
+       gemm_h_ok<L_RK, L_RK>(c, c->dz2, c->ldAH2, P(c, c->theta, L.a[AW2]), c->AH2, B, c->AH1,
+                             c->AH2, 1, &kh))
+          ? act_twin(c, c->dz2)
+          : Twin();
+  const Twin dz1t =
+      gemm_h_ok<L_KR, L_KR>(c, c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1, B, 0, &kh)
+          ? act_twin(c, c->dz1)
+          : Twin();
   TkPart tp = tk_part(c->dz3, c->ldA, c->A, P(c, c->theta, L.a[AW3]), c->A, 1, c->AH2, nullptr,
-                      0, c->dz2, c->ldAH2);
+                      0, dz2t.p ? nullptr : c->dz2, c->ldAH2);
+  tp.outh = dz2t.p;
+  tp.hps = dz2t.ps;
+  tp.hnp = c->hnp;
   tp.aux = c->h2;
   tp.ldaux = c->ldAH2;
   tp.colsum = c->colpart;
@@ -1042,7 +1084,10 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
     e.post = 1;
     e.aux = c->h2;
     e.ldaux = c->ldAH2;
-    e.out = c->dz2;
+    e.out = dz2t.p ? nullptr : c->dz2;
+    e.outh = dz2t.p;
+    e.h_plane_stride = dz2t.ps;
+    e.h_planes = c->hnp;
     e.ldo = c->ldAH2;
     e.colsum = c->colpart;
     e.ld_colsum = c->AH2;
@@ -1060,7 +1105,7 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   e.ldo = c->AH2;
   e.out_split_stride = (long long)c->AH1 * c->AH2;
   GemmPlan pW2 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1,
-                                         c->AH2, B, e, 0, c->split_cap_W2);
+                                         c->AH2, B, e, 0, c->split_cap_W2, G + L.a[AW2].off);
   c->cur = main;
   // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
   float* colpart1 = c->colpart + (size_t)mt2 * c->AH2;
@@ -1068,7 +1113,10 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   e.post = 1;
   e.aux = c->h1;
   e.ldaux = c->ldAH1;
-  e.out = c->dz1;
+  e.out = dz1t.p ? nullptr : c->dz1;
+  e.outh = dz1t.p;
+  e.h_plane_stride = dz1t.ps;
+  e.h_planes = c->hnp;
   e.ldo = c->ldAH1;
   e.colsum = colpart1;
   e.ld_colsum = c->AH1;
@@ -1080,18 +1128,15 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   e.ldo = c->AH1;
   e.out_split_stride = (long long)c->S * c->AH1;
   GemmPlan pW1 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1,
-                                         B, e, 0, c->split_cap_W1);
+                                         B, e, 0, c->split_cap_W1, G + L.a[AW1].off);
   if (par) fork_to(c, 3, c->aux[0], main);  // join dW3, dW2
   ReduceTable tab;
   tab.nseg = 0;
-  add_seg(tab, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1, pW1.splits,
-          (long long)c->S * c->AH1);
+  add_wgrad(tab, pW1, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1);
   add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, pz1.mt(B), c->AH1);
-  add_seg(tab, c->slab_W2, G + L.a[AW2].off, (long long)c->AH1 * c->AH2, pW2.splits,
-          (long long)c->AH1 * c->AH2);
+  add_wgrad(tab, pW2, c->slab_W2, G + L.a[AW2].off, (long long)c->AH1 * c->AH2);
   add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt2, c->AH2);
-  add_seg(tab, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A, pW3.splits,
-          (long long)c->AH2 * c->A);
+  add_wgrad(tab, pW3, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.actor_begin, L.actor_end - L.actor_begin);
   adam_launch(c, 0, !fused);

@@ -223,7 +223,7 @@ __global__ void critic_head_bwd_kernel(const float* __restrict__ h, int ldh,
 // column quads x 4 row groups of a chunk (16-B loads / stores, several rows
 // in flight per thread), the groups' partial sums combined in LDS in a fixed
 // order; also writes dh_pre's bf16 twin (dtw, tnp planes tps apart) for the
-// bf16-operand GEMMs that read it.
+// bf16-operand GEMMs that read it (dh_pre may be null: twin only).
 __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
     const float* __restrict__ h, int ldh, const float* __restrict__ dq,
     const float* __restrict__ Wo, int B, int H2, int rows_per_chunk, float* __restrict__ dh_pre,
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
       dp.y = __fmul_rn(__fmul_rn(d, w.y), elu_grad_factor(hv.y));
       dp.z = __fmul_rn(__fmul_rn(d, w.z), elu_grad_factor(hv.z));
       dp.w = __fmul_rn(__fmul_rn(d, w.w), elu_grad_factor(hv.w));
-      *reinterpret_cast<float4*>(dh_pre + (size_t)b * ld_dh + j) = dp;
+      if (dh_pre) *reinterpret_cast<float4*>(dh_pre + (size_t)b * ld_dh + j) = dp;
       if (dtw) store_twin4(dtw + (size_t)b * ld_dh + j, tps, tnp, dp);
       sw.x = fmaf(hv.x, d, sw.x);
       sw.y = fmaf(hv.y, d, sw.y);
