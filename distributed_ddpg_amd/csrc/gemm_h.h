@@ -23,9 +23,21 @@
 // lane's SOURCE address.  Rows / columns past M or N are clamped (their
 // outputs are discarded by the epilogue); K must be a multiple of BK per split.
 #pragma once
+#include <type_traits>
+#include <utility>
 #include "gemm_bf16.h"
 
 namespace ddpg {
+
+// f(std::integral_constant<int, 0>{}) ... f(std::integral_constant<int, N-1>{})
+template <typename F, int... I>
+DDPG_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+DDPG_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 struct GemmHArgs {
   const __bf16* A;
@@ -147,10 +159,27 @@ DDPG_DEV void hg_wait(bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
   }
 }
 
+// Main loop (software-pipelined across k-tiles; every phase boundary is a
+// sched_barrier so hipcc cannot sink the MFMAs below the next step's waits):
+//   k-step ks < KS-1: wait own reads of ks | issue reads of ks+1 | MFMAs of ks,
+//                     with this tile's share of the tile-(t+2) glds between them
+//   k-step KS-1:      wait own reads | vmcnt (tile t+1 landed) | s_barrier |
+//                     issue reads of tile t+1 k-step 0 | MFMAs of KS-1
+// so the barrier and the next tile's first LDS reads sit under one k-step of
+// MFMAs.  Ring of 3 LDS stages: tile t+2 is staged into tile t-1's buffer,
+// whose reads every wave finished before the barrier that ended tile t-1.
+//
+// Measured alternative (tools/gemmh_bench.hip, round 2): one tile in flight
+// with waves 4-7 staggered KS/2 k-steps behind waves 0-3 (so SIMD partners
+// are in different phases) is 15-25 % SLOWER on every C3/C5 shape than two
+// tiles in flight without a stagger: the glds latency under full load, not
+// the phase pairing, is what the second tile in flight covers.
 template <int AL, int BL, int NP, int BM, int BK>
 __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   using C = HgCfg<BM, BK, NP>;
   constexpr int TM = BM / 64;
+  constexpr int KS = BK / 16;
+  static_assert(KS % 2 == 0, "fragment register sets alternate by k-step parity");
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM_BYTES / 4];
   char* const lds = reinterpret_cast<char*>(smem);
 
@@ -169,6 +198,15 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+  // NP = 3: the five small plane products go to their own accumulators, so
+  // the main (hh) chain takes one rounding per k-step instead of six
+  f32x16 acs[NP == 3 ? TM : 1];
+  if constexpr (NP == 3) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acs[i][r] = 0.f;
+  }
 
   const __bf16* sa[C::A_PW];
   const __bf16* sb[C::B_PW];
@@ -181,38 +219,26 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   const long long stepA = AL == L_RK ? BK : (long long)BK * g.lda;
   const long long stepB = BL == L_RK ? BK : (long long)BK * g.ldb;
 
-  // issue k-tile t's loads into stage buffer `buf` (G glds per wave)
-  auto stage = [&](int t, int buf) {
+  // glds piece q (0 .. G-1) of k-tile t into stage buffer `buf`
+  auto piece = [&](int t, int buf, int q) {
     char* base = lds + buf * C::STAGE;
+    const int p = q / (C::A_PW + C::B_PW), r = q % (C::A_PW + C::B_PW);
+    if (r < C::A_PW)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(sa[r] + p * g.pa + t * stepA),
+          (lds_void*)(base + p * C::A_BYTES + (wave * C::A_PW + r) * 1024), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(sb[r - C::A_PW] + p * g.pb + t * stepB),
+          (lds_void*)(base + NP * C::A_BYTES + p * C::B_BYTES +
+                      (wave * C::B_PW + r - C::A_PW) * 1024),
+          16, 0, 0);
+  };
+  auto stage = [&](int t, int buf) {
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-#pragma unroll
-      for (int i = 0; i < C::A_PW; ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const void*)(sa[i] + p * g.pa + t * stepA),
-            (lds_void*)(base + p * C::A_BYTES + (wave * C::A_PW + i) * 1024), 16, 0, 0);
-#pragma unroll
-      for (int i = 0; i < C::B_PW; ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const void*)(sb[i] + p * g.pb + t * stepB),
-            (lds_void*)(base + NP * C::A_BYTES + p * C::B_BYTES + (wave * C::B_PW + i) * 1024),
-            16, 0, 0);
-    }
+    for (int q = 0; q < C::G; ++q) piece(t, buf, q);
   };
 
-  // R fragment reads per k-step; the counted waits below must fit the 4-bit
-  // lgkmcnt.
-  constexpr int RA = AL == L_RK ? 1 : 2, RB = BL == L_RK ? 1 : 2;
-  constexpr int R = NP * (TM * RA + RB);
-  // NP = 3: the five small plane products go to their own accumulators, so
-  // the main (hh) chain takes one rounding per k-step instead of six
-  f32x16 acs[NP == 3 ? TM : 1];
-  if constexpr (NP == 3) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acs[i][r] = 0.f;
-  }
   auto read = [&](const char* base, int ks, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -222,67 +248,90 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
         av[p][i] = hg_frag<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 32 * i, ks, lane);
     }
   };
-  auto mfmas = [&](bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if constexpr (NP == 3) {
-        // small terms, smallest first: lh, mm, hl, mh, hm  (planes 0 = h, 1 = m, 2 = l)
-        f32x16 c = acs[i];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
-        acs[i] = c;
-      }
-      acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
+  auto mfma_i = [&](int i, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+    if constexpr (NP == 3) {
+      // small terms, smallest first: lh, mm, hl, mh, hm  (planes 0 = h, 1 = m, 2 = l)
+      f32x16 c = acs[i];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
+      acs[i] = c;
     }
-  };
-  // k-step fragments are read DEPTH steps ahead of their MFMAs (a ring of
-  // DEPTH + 1 register sets; counted lgkmcnt, LDS reads return in order).
-  constexpr int KS = BK / 16;
-  constexpr int DEPTH = (2 * R <= 15 && KS > 2) ? 2 : (R <= 15 ? 1 : 0);
-  auto compute = [&](int buf) {
-    const char* base = lds + buf * C::STAGE;
-    bf16x8 fa[DEPTH + 1][NP][TM], fb[DEPTH + 1][NP];
-#pragma unroll
-    for (int ks = 0; ks < DEPTH; ++ks) read(base, ks, fa[ks], fb[ks]);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      constexpr int NS = DEPTH + 1;
-      if (ks + DEPTH < KS) read(base, ks + DEPTH, fa[(ks + DEPTH) % NS], fb[(ks + DEPTH) % NS]);
-      const int ahead = (ks + DEPTH < KS ? DEPTH : KS - 1 - ks);  // steps issued after ks
-      if (ahead == 2)
-        hg_wait<(2 * R <= 15 ? 2 * R : 0)>(fa[ks % NS], fb[ks % NS]);
-      else if (ahead == 1)
-        hg_wait<(R <= 15 ? R : 0)>(fa[ks % NS], fb[ks % NS]);
-      else
-        hg_wait<0>(fa[ks % NS], fb[ks % NS]);
-      mfmas(fa[ks % NS], fb[ks % NS]);
-    }
+    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
   };
 
-  // 3-stage ring: at iteration t, tiles t and t+1 are in flight; wait for t
-  // (this wave's loads), barrier (everyone's loads of t landed, everyone's
-  // reads of t-1 done), refill t-1's buffer with t+2, consume t.
+  bf16x8 fa[2][NP][TM], fb[2][NP];
+  // glds of the next-but-one tile are spread over the first KS-1 k-steps
+  constexpr int GSEG = KS - 1;
+  // one k-tile; STAGE_NEXT2: stage tile t+2; HAS_NEXT: tile t+1 exists
+  auto tile = [&](int t, auto stage_c, auto next_c) {
+    constexpr bool STAGE_NEXT2 = decltype(stage_c)::value;
+    constexpr bool HAS_NEXT = decltype(next_c)::value;
+    const char* base = lds + (t % HG_STAGES) * C::STAGE;
+    const int sbuf = (t + 2) % HG_STAGES;
+    static_for<KS>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      auto& av = fa[ks & 1];
+      auto& bv = fb[ks & 1];
+      hg_wait<0, NP, TM>(av, bv);
+      if constexpr (ks + 1 < KS) {
+        read(base, ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+      } else if constexpr (HAS_NEXT) {
+        if constexpr (STAGE_NEXT2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read(lds + ((t + 1) % HG_STAGES) * C::STAGE, 0, fa[0], fb[0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) mfma_i(i, av, bv);
+      if constexpr (STAGE_NEXT2 && ks < GSEG) {
+        constexpr int lo = ks * C::G / GSEG, hi = (ks + 1) * C::G / GSEG;
+#pragma unroll
+        for (int q = lo; q < hi; ++q) piece(t + 2, sbuf, q);
+        // MFMAs and glds alternate (MPG MFMAs, one glds, ...)
+        constexpr int NM = TM * (NP == 3 ? 6 : 1), NG = hi - lo;
+        constexpr int MPG = NG > 0 ? NM / NG : NM;
+        static_for<NG>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, MPG, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        });
+        if constexpr (NM - MPG * NG > 0)
+          __builtin_amdgcn_sched_group_barrier(0x008, NM - MPG * NG, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
   if (nk > 0) {
     stage(0, 0);
-    if (nk > 1) stage(1, 1);
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (t + 2 < nk) stage(t + 2, (t + 2) % HG_STAGES);
-      compute(t % HG_STAGES);
+    if (nk > 1) {
+      stage(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(lds, 0, fa[0], fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    int t = 0;
+    for (; t + 2 < nk; ++t) tile(t, T_{}, T_{});
+    if (t + 1 < nk) tile(t++, F_{}, T_{});
+    tile(t, F_{}, F_{});
   }
   if constexpr (NP == 3) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] += acs[i];
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // staging buffers are reused by the epilogue
   GemmArgs ge;
   ge.M = g.M;
