@@ -421,6 +421,7 @@ static void twins_refresh(ddpg_ctx* c) {
 
 // env DDPG_GEMM_H=0 keeps every GEMM off the bf16-twin kernel
 static int g_gemm_h = -1;
+static int g_gemm_mf = -1;
 
 template <int AL, int BL, int VA, int VB>
 static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const GemmArgs& g) {
@@ -532,13 +533,22 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       a.xcd = g_xcd_remap;
       a.e = ee;
       static const char* lay[2] = {"RK", "KR"};
+      // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
+      if (g_gemm_mf < 0) {
+        const char* v = getenv("DDPG_GEMM_MF");
+        g_gemm_mf = (v && atoi(v) == 32) ? 32 : 16;
+      }
+      const bool h16 = c->hnp == 1 && g_gemm_mf == 16;
       char key[112];
-      snprintf(key, sizeof key, "gemm_h_kernel<%s,%s,NP=%d>|%s", lay[AL], lay[BL], c->hnp, name);
+      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s", h16 ? "gemm_h16_kernel" : "gemm_h_kernel",
+               lay[AL], lay[BL], c->hnp, name);
       ProfScope ps(c, key, 2.0 * M * N * (double)K,
                    2.0 * c->hnp * ((double)M * K + (double)K * N) +
                        4.0 * (double)M * N * h.splits);
       const dim3 grid(h.nt(N), h.mt(M), h.splits);
-      if (c->hnp == 1)
+      if (h16)
+        hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
+      else if (c->hnp == 1)
         hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else
         hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 3, 128, 32>), grid, dim3(HG_NT), 0, c->cur, a);

@@ -113,35 +113,59 @@ DDPG_DEV void gemm_epilogue_barriers(const GemmEpi& e) {
   if (e.colsum) __syncthreads();
 }
 
+// Row / column (within the wave's 32x32 block) of accumulator register r of
+// lane l: MF = 32 is the v_mfma_f32_32x32x* layout; MF = 16 is four 16x16
+// tiles packed as register 4 (2 tr + tc) + q = row 16 tr + 4 (l >> 4) + q,
+// column 16 tc + (l & 15) (gemm_h16_kernel).
+template <int MF>
+DDPG_DEV int acc_row(int r, int lane) {
+  return MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+                  : 16 * (r >> 3) + 4 * (lane >> 4) + (r & 3);
+}
+template <int MF>
+DDPG_DEV int acc_col(int r, int lane) {
+  return MF == 32 ? (lane & 31) : 16 * ((r >> 2) & 1) + (lane & 15);
+}
+
 // Element-wise part of the epilogue on one wave's accumulators, specialised
 // on the flag combinations the learner uses (BIAS: + bias[n]; ACT 1: elu;
 // POST 1: * EluGrad factor of aux[m][n]; POST 2: pw[n] * EluGrad factor of v).
 // Values outside the M x N range become 0 (they feed the row reductions).
-template <int BM, int BN, int WGN, bool BIAS, int ACT, int POST>
+template <int BM, int BN, int WGN, bool BIAS, int ACT, int POST, int MF>
 DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& e, int M, int N,
-                        int n0, int m0, int wm, int wn, int h, int li) {
+                        int n0, int m0, int wm, int wn, int lane) {
   constexpr int TM = BM / 64, TN = BN / (32 * WGN);
   constexpr int WR = BM / 2, WC = BN / WGN;
+  constexpr int NC = MF == 32 ? 1 : 2;  // distinct columns per lane in a block
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WC + j * 32 + li;
-      const bool nok = n < N;
-      const float bn = (BIAS && nok) ? e.bias[n] : 0.f;
-      const float pwn = (POST == 2 && nok) ? e.pw[n] : 0.f;
+      int ncol[NC];
+      float bnc[NC], pwc[NC];
+#pragma unroll
+      for (int u = 0; u < NC; ++u) {
+        ncol[u] = n0 + wn * WC + j * 32 + acc_col<MF>(4 * u, lane);
+        bnc[u] = (BIAS && ncol[u] < N) ? e.bias[ncol[u]] : 0.f;
+        pwc[u] = (POST == 2 && ncol[u] < N) ? e.pw[ncol[u]] : 0.f;
+      }
       float av[16];
       if constexpr (POST == 1) {  // all 16 loads in flight before the first use
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float* q = (nok && m < M) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
+          const int n = ncol[NC == 1 ? 0 : (r >> 2) & 1];
+          const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
+          const float* q = (n < N && m < M) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
           av[r] = *q;
         }
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int u = NC == 1 ? 0 : (r >> 2) & 1;
+        const int n = ncol[u];
+        const bool nok = n < N;
+        const float bn = bnc[u], pwn = pwc[u];
+        const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
         float v = acc[i][j][r];
         if constexpr (BIAS) v = __fadd_rn(v, bn);
         if constexpr (ACT == 1) v = elu_f(v);
@@ -168,7 +192,7 @@ DDPG_DEV void store_twin(const GemmEpi& e, size_t i, float4 v) {
 // wave row (BM/2 rows) at a time, from where it is stored as float4 rows
 // (1 KiB per wave instruction instead of 128-B column pieces) and reduced
 // (bias-gradient column sums, thin projections).
-template <int BM, int BN, int WGN = 2>
+template <int BM, int BN, int WGN = 2, int MF = 32>
 DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem,
                             const GemmArgs& g,
                             int tid, int n0, int m0, int z, int bx, int by) {
@@ -178,22 +202,21 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   constexpr int WR = BM / 2, WC = BN / WGN;
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int h = lane >> 5, li = lane & 31;
   const GemmEpi& e = g.e;
   const int M = g.M, N = g.N;
   float* outp = e.out ? e.out + (size_t)z * e.out_split_stride : nullptr;
 
   const bool bias = e.bias != nullptr;
   if (!bias && e.act == 0 && e.post == 0)
-    epi_apply<BM, BN, WGN, false, 0, 0>(acc, e, M, N, n0, m0, wm, wn, h, li);
+    epi_apply<BM, BN, WGN, false, 0, 0, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (bias && e.act == 1 && e.post == 0)
-    epi_apply<BM, BN, WGN, true, 1, 0>(acc, e, M, N, n0, m0, wm, wn, h, li);
+    epi_apply<BM, BN, WGN, true, 1, 0, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (bias && e.act == 1 && e.post == 2)
-    epi_apply<BM, BN, WGN, true, 1, 2>(acc, e, M, N, n0, m0, wm, wn, h, li);
+    epi_apply<BM, BN, WGN, true, 1, 2, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (!bias && e.act == 0 && e.post == 1)
-    epi_apply<BM, BN, WGN, false, 0, 1>(acc, e, M, N, n0, m0, wm, wn, h, li);
+    epi_apply<BM, BN, WGN, false, 0, 1, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (bias && e.act == 0 && e.post == 0)
-    epi_apply<BM, BN, WGN, true, 0, 0>(acc, e, M, N, n0, m0, wm, wn, h, li);
+    epi_apply<BM, BN, WGN, true, 0, 0, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
   else  // not used by the learner; the host rejects other combinations
     __builtin_trap();
 
@@ -226,8 +249,8 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int rl = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            Vs[rl * VS_LD + wn * WC + j * 32 + li] = acc[i][j][r];
+            const int rl = i * 32 + acc_row<MF>(r, lane);
+            Vs[rl * VS_LD + wn * WC + j * 32 + acc_col<MF>(r, lane)] = acc[i][j][r];
           }
     }
     __syncthreads();

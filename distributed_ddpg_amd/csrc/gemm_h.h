@@ -69,10 +69,15 @@ struct HgCfg {
 
 // RK image: rows of 2*BK bytes; chunk swizzle spreading 16 consecutive rows
 // over the 16 slots of a 256-B bank row
-template <int BK>
+// MF = 16 (16x16x32 fragments: lane l reads row l & 15, 16-B chunk l >> 4 of
+// the 32-k step) at BK = 32 needs a different spread over the ds_read_b128
+// lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...: (row >> 2) & 2.
+template <int BK, int MF = 32>
 DDPG_DEV int rk_swz(int row) {
   if constexpr (BK == 64)
     return (row >> 1) & 7;
+  else if constexpr (MF == 16)
+    return (row >> 2) & 2;
   else
     return (row >> 2) & 3;
 }
@@ -81,14 +86,14 @@ DDPG_DEV int kr_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 // Source address of this lane's 16 B of piece `piece` (1 KiB of the image).
 // R = row extent of the operand (M or N), r0 = the block's first row,
 // BR = image rows (BM or 128).
-template <int L, int BR, int BK>
+template <int L, int BR, int BK, int MF = 32>
 DDPG_DEV const __bf16* hg_src(const __bf16* P, int ld, int R, int r0, int kbeg, int piece,
                               int lane) {
   const int off = piece * 1024 + 16 * lane;
   if constexpr (L == L_RK) {
     constexpr int RB = 2 * BK;
     const int row = off / RB, pc = (off % RB) >> 4;
-    const int c = pc ^ rk_swz<BK>(row);
+    const int c = pc ^ rk_swz<BK, MF>(row);
     const int gr = min(r0 + row, R - 1);
     return P + (size_t)gr * ld + kbeg + 8 * c;
   } else {
@@ -146,6 +151,28 @@ DDPG_DEV bf16x8 hg_frag(const char* img, int rb, int ks, int lane) {
   }
 }
 
+// 16x16x32 MFMA fragment (lane: row/col l & 15 of the operand tile starting
+// at image row `rb`, k = 32 ks + 8 (l >> 4) .. +7).  KR: the same
+// ds_read_b64_tr_b16 pair as hg_frag, with the four 16-lane groups on four
+// k-row octets (conflict-free under kr_swz).
+template <int L, int BK>
+DDPG_DEV bf16x8 hg_frag16(const char* img, int rb, int ks, int lane) {
+  if constexpr (L == L_RK) {
+    const int r = rb + (lane & 15);
+    const int c = (4 * ks + (lane >> 4)) ^ rk_swz<BK, 16>(r);
+    return b128_read(img + r * (2 * BK) + 16 * c);
+  } else {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int col = rb + 4 * p;
+    const char* sub = img + (col >> 7) * (BK * 256);
+    const int ch = (col & 127) >> 3;
+    const int k0 = 32 * ks + 8 * (lane >> 4) + q, k1 = k0 + 4;
+    const char* a0 = sub + k0 * 256 + 16 * (ch ^ kr_swz(k0)) + 8 * (p & 1);
+    const char* a1 = sub + k1 * 256 + 16 * (ch ^ kr_swz(k1)) + 8 * (p & 1);
+    return __builtin_shufflevector(tr_read(a0), tr_read(a1), 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
 // lgkmcnt(0) tied to the fragments, so no MFMA reading them is scheduled
 // above the wait
 template <int N, int NP, int TM>
@@ -156,6 +183,17 @@ DDPG_DEV void hg_wait(bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
     asm volatile("" : "+v"(bv[p]));
 #pragma unroll
     for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av[p][i]));
+  }
+}
+template <int NP, int TA, int TB>
+DDPG_DEV void hg_wait16(bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int j = 0; j < TB; ++j) asm volatile("" : "+v"(bv[p][j]));
+#pragma unroll
+    for (int i = 0; i < TA; ++i) asm volatile("" : "+v"(av[p][i]));
   }
 }
 
@@ -338,6 +376,209 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   ge.N = g.N;
   ge.e = g.e;
   gemm_epilogue<BM, HG_BN, 4>(acc, smem, ge, tid, n0, m0, z, bx, by);
+}
+
+// The same GEMM on v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md "DVFS
+// give-back" item 7: at equal cycles per FLOP the chip holds a higher clock on
+// the 16x16 shape under random data).  Wave tile (BM/2) x 32 = TA x 2 16x16
+// tiles; one 32-deep k-step per 32 of BK (KS32 = BK / 32).  Schedule as in
+// gemm_h_kernel: k-step j waits its own reads, issues j+1's, then its MFMAs;
+// the tile barrier X_t sits in the last k-step of tile t behind the reads of
+// tile t.  Because every fragment of tile t is in registers once X_t is passed,
+// tile t's buffer is free then: glds of tile t+3 go there right after X_t
+// (three buffers: t+1 being read, t+2 in flight, t+3 issued), interleaved with
+// the MFMAs of that last k-step.  The accumulators are repacked into the 32x32
+// register layout of gemm_epilogue<..., 16> (see acc_row / acc_col there).
+template <int AL, int BL, int NP, int BM, int BK>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h16_kernel(GemmHArgs g) {
+  using C = HgCfg<BM, BK, NP>;
+  constexpr int TM = BM / 64;        // 32-row blocks per wave (epilogue layout)
+  constexpr int TA = BM / 32;        // 16-row A fragments per wave
+  constexpr int TB = 2;              // 16-column B fragments per wave
+  constexpr int KS = BK / 32;
+  // NP = 3 holds 2 x 3 planes x 6 fragments of a 32-deep step: past 256 VGPRs
+  // (it spilled to scratch), so the fp32 configuration keeps gemm_h_kernel
+  static_assert(NP == 1, "16x16x32 variant: one plane (bf16 configuration) only");
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM_BYTES / 4];
+  char* const lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int bx, by;
+  xcd_tile(bx, by, g.xcd);
+  const int n0 = bx * HG_BN, m0 = by * BM, z = blockIdx.z;
+  const int kbeg = z * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+
+  f32x4 acc[TA][TB], acs[NP == 3 ? TA : 1][TB];
+#pragma unroll
+  for (int i = 0; i < TA; ++i)
+#pragma unroll
+    for (int j = 0; j < TB; ++j) {
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (NP == 3) acs[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  const __bf16* sa[C::A_PW];
+  const __bf16* sb[C::B_PW];
+#pragma unroll
+  for (int i = 0; i < C::A_PW; ++i)
+    sa[i] = hg_src<AL, BM, BK, 16>(g.A, g.lda, g.M, m0, kbeg, wave * C::A_PW + i, lane);
+#pragma unroll
+  for (int i = 0; i < C::B_PW; ++i)
+    sb[i] = hg_src<BL, HG_BN, BK, 16>(g.B, g.ldb, g.N, n0, kbeg, wave * C::B_PW + i, lane);
+  const long long stepA = AL == L_RK ? BK : (long long)BK * g.lda;
+  const long long stepB = BL == L_RK ? BK : (long long)BK * g.ldb;
+
+  auto piece = [&](int t, int buf, int q) {
+    char* base = lds + buf * C::STAGE;
+    const int p = q / (C::A_PW + C::B_PW), r = q % (C::A_PW + C::B_PW);
+    if (r < C::A_PW)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(sa[r] + p * g.pa + t * stepA),
+          (lds_void*)(base + p * C::A_BYTES + (wave * C::A_PW + r) * 1024), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(sb[r - C::A_PW] + p * g.pb + t * stepB),
+          (lds_void*)(base + NP * C::A_BYTES + p * C::B_BYTES +
+                      (wave * C::B_PW + r - C::A_PW) * 1024),
+          16, 0, 0);
+  };
+  auto stage = [&](int t, int buf) {
+#pragma unroll
+    for (int q = 0; q < C::G; ++q) piece(t, buf, q);
+  };
+  auto read = [&](const char* base, int ks, bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int j = 0; j < TB; ++j)
+        bv[p][j] = hg_frag16<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * 32 + 16 * j,
+                                     ks, lane);
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+        av[p][i] = hg_frag16<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 16 * i, ks, lane);
+    }
+  };
+  auto mfma_all = [&](bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) {
+        if constexpr (NP == 3) {
+          // small terms, smallest first: lh, mm, hl, mh, hm
+          f32x4 c = acs[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], c, 0, 0, 0);
+          acs[i][j] = c;
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+      }
+  };
+
+  bf16x8 fa[2][NP][TA], fb[2][NP][TB];
+  constexpr int NM = TA * TB * (NP == 3 ? 6 : 1);  // MFMAs per k-step
+  // one k-tile whose first k-step uses register set P0; STAGE3: stage tile
+  // t+3 after X_t; NEXT: tile t+1 exists; G2: tile t+2 was staged (vmcnt(G))
+  auto tile = [&](int t, auto p0_c, auto stage_c, auto next_c, auto g2_c) {
+    constexpr int P0 = decltype(p0_c)::value;
+    constexpr bool STAGE3 = decltype(stage_c)::value;
+    constexpr bool NEXT = decltype(next_c)::value;
+    constexpr bool G2 = decltype(g2_c)::value;
+    const char* base = lds + (t % HG_STAGES) * C::STAGE;
+    static_for<KS>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      constexpr int cs = (P0 + ks) & 1, ns = (P0 + ks + 1) & 1;
+      hg_wait16<NP, TA, TB>(fa[cs], fb[cs]);
+      if constexpr (ks + 1 < KS) {
+        read(base, ks + 1, fa[ns], fb[ns]);
+      } else if constexpr (NEXT) {
+        if constexpr (G2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read(lds + ((t + 1) % HG_STAGES) * C::STAGE, 0, fa[ns], fb[ns]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_all(fa[cs], fb[cs]);
+      if constexpr (ks + 1 == KS && STAGE3) {
+        stage(t + 3, t % HG_STAGES);
+        constexpr int NG = C::G, MPG = NM / NG > 0 ? NM / NG : 1;
+        static_for<NG>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, MPG, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        });
+        if constexpr (NM - MPG * NG > 0)
+          __builtin_amdgcn_sched_group_barrier(0x008, NM - MPG * NG, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  // tile t with its register-set parity (KS odd: sets alternate per tile)
+  auto run = [&](int t, auto stage_c, auto next_c, auto g2_c) {
+    if constexpr (KS % 2 == 0) {
+      tile(t, std::integral_constant<int, 0>{}, stage_c, next_c, g2_c);
+    } else {
+      if (t & 1)
+        tile(t, std::integral_constant<int, 1>{}, stage_c, next_c, g2_c);
+      else
+        tile(t, std::integral_constant<int, 0>{}, stage_c, next_c, g2_c);
+    }
+  };
+
+  if (nk > 0) {
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    if (nk > 2) {
+      stage(2, 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::G) : "memory");
+    } else if (nk > 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(lds, 0, fa[0], fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    int t = 0;
+    for (; t + 3 < nk; ++t) run(t, T_{}, T_{}, T_{});   // stages t+3; t+2 in flight
+    if (t + 2 < nk) run(t++, F_{}, T_{}, T_{});          // t+2 in flight
+    if (t + 1 < nk) run(t++, F_{}, T_{}, F_{});
+    run(t, F_{}, F_{}, F_{});
+  }
+  // repack into the 32x32 register layout: 32-row block i = fragments 2i, 2i+1;
+  // register 4 (2 tr + tc) + q of block i = row 16 tr + 4 (l >> 4) + q,
+  // column 16 tc + (l & 15)
+  f32x16 out[TM][1];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = acc[2 * i + tr][tc][q];
+          if constexpr (NP == 3) v += acs[2 * i + tr][tc][q];
+          out[i][0][4 * (2 * tr + tc) + q] = v;
+        }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // staging buffers are reused by the epilogue
+  GemmArgs ge;
+  ge.M = g.M;
+  ge.N = g.N;
+  ge.e = g.e;
+  gemm_epilogue<BM, HG_BN, 4, 16>(out, smem, ge, tid, n0, m0, z, bx, by);
 }
 
 }  // namespace ddpg

@@ -41,9 +41,9 @@ def bench_name(rocprof_name):
     if sym == "gemm_s3_kernel" and len(a) == 3:
         # bench.py labels the one-plane instantiation gemm_bf16_kernel
         return "%s<%s,%s>" % ("gemm_s3_kernel" if a[2] == "3" else "gemm_bf16_kernel", a[0], a[1])
-    if sym == "gemm_h_kernel" and len(a) >= 3:
+    if sym in ("gemm_h_kernel", "gemm_h16_kernel") and len(a) >= 3:
         # bench.py labels it by operand layouts and plane count
-        return "gemm_h_kernel<%s,%s,NP=%s>" % (a[0], a[1], a[2])
+        return "%s<%s,%s,NP=%s>" % (sym, a[0], a[1], a[2])
     return "%s<%s>" % (sym, ",".join(a))
 
 

@@ -73,7 +73,7 @@ struct Case {
 static float *gA, *gB, *gC, *gR;
 static __bf16 *hA, *hB;
 
-template <int AL, int BL, int NP, int BM, int BK>
+template <int AL, int BL, int NP, int BM, int BK, int MF>
 static void run_case(const Case& c) {
   const size_t na = (size_t)c.M * c.K, nb = (size_t)c.K * c.N, nc = (size_t)c.M * c.N;
   // fresh operands (NP = 1 rounds them), planes
@@ -121,7 +121,12 @@ static void run_case(const Case& c) {
   g.e.ldo = c.N;
   g.e.out_split_stride = (long long)nc;
   dim3 grid((c.N + HG_BN - 1) / HG_BN, (c.M + BM - 1) / BM, c.splits);
-  auto f = [&] { hipLaunchKernelGGL((gemm_h_kernel<AL, BL, NP, BM, BK>), grid, dim3(HG_NT), 0, 0, g); };
+  auto f = [&] {
+    if constexpr (MF == 16)
+      hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, NP, BM, BK>), grid, dim3(HG_NT), 0, 0, g);
+    else
+      hipLaunchKernelGGL((gemm_h_kernel<AL, BL, NP, BM, BK>), grid, dim3(HG_NT), 0, 0, g);
+  };
   const float us = time_it(f, 10);
   // check: sum the split slabs on the host
   std::vector<float> out(nc * c.splits), ref(nc);
@@ -157,18 +162,24 @@ static void run_case(const Case& c) {
   const double flop = 2.0 * c.M * c.N * (double)c.K;
   const double tf = flop / (us * 1e-6) / 1e12;
   const double peak = NP == 3 ? 2500.0 / 6 : 2500.0;
-  printf("%-34s NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d  %8.2f us %7.1f TF (%5.1f%% of %.0f)  "
+  printf("%-26s MF%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d  %8.2f us %7.1f TF (%5.1f%% of %.0f)  "
          "vs f32 %.2e | vs f64: gemm_h %.2e, f32 MFMA %.2e\n",
-         c.name, NP, BM, BK, c.M, c.N, c.K, c.splits, us, tf, 100.0 * tf / peak, peak,
+         c.name, MF, NP, BM, BK, c.M, c.N, c.K, c.splits, us, tf, 100.0 * tf / peak, peak,
          maxerr / maxref, e64h / m64, e64r / m64);
   fflush(stdout);
 }
 
+template <int NP, int BM, int BK, int MF>
+static void dispatch1(const Case& c) {
+  if (c.al == L_RK && c.bl == L_KR) run_case<L_RK, L_KR, NP, BM, BK, MF>(c);
+  if (c.al == L_RK && c.bl == L_RK) run_case<L_RK, L_RK, NP, BM, BK, MF>(c);
+  if (c.al == L_KR && c.bl == L_KR) run_case<L_KR, L_KR, NP, BM, BK, MF>(c);
+}
+// the 32x32x16 and the 16x16x32 kernel on the same case, interleaved
 template <int NP, int BM, int BK>
 static void dispatch(const Case& c) {
-  if (c.al == L_RK && c.bl == L_KR) run_case<L_RK, L_KR, NP, BM, BK>(c);
-  if (c.al == L_RK && c.bl == L_RK) run_case<L_RK, L_RK, NP, BM, BK>(c);
-  if (c.al == L_KR && c.bl == L_KR) run_case<L_KR, L_KR, NP, BM, BK>(c);
+  dispatch1<NP, BM, BK, 32>(c);
+  if constexpr (NP == 1) dispatch1<NP, BM, BK, 16>(c);
 }
 
 int main(int argc, char** argv) {

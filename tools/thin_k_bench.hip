@@ -39,12 +39,13 @@ using namespace ddpg;
 
 typedef void (*tk_fn)(TkArgs);
 static tk_fn g_kern = thin_k_kernel;
+static int g_rb = 0;  // row blocks of the kernel under test
 static float time_it(const TkArgs& a, int nparts, int reps) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   int nmax = std::max(a.p[0].N, nparts > 1 ? a.p[1].N : 0);
-  dim3 grid((nmax + TK_COLS - 1) / TK_COLS, (a.M + TK_ROWS - 1) / TK_ROWS, nparts);
+  dim3 grid((nmax + TK_COLS - 1) / TK_COLS, g_rb, nparts);
   for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(g_kern, grid, dim3(TK_NT), 0, 0, a);
   hipEventRecord(e0);
   for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(g_kern, grid, dim3(TK_NT), 0, 0, a);
@@ -58,10 +59,12 @@ static float time_it(const TkArgs& a, int nparts, int reps) {
 static void run_all();
 int main() {
   printf("== new thin_k_kernel\n");
+  g_rb = 4096 / TK_ROWS;
   run_all();
 #ifdef WITH_OLD
   printf("== old thin_k_kernel\n");
-  g_kern = thin_k_old_kernel;
+  g_kern = old::thin_k_old_kernel;
+  g_rb = 4096 / 64;
   run_all();
 #endif
   return 0;
@@ -89,17 +92,30 @@ static void run_all() {
   a.M = M;
   a.p[0] = p;
   printf("K64 bias+elu+store           %.2f us\n", time_it(a, 1, 200));
-  phases("K64", 8 * 128);
+  phases("K64", 8 * g_rb);
+  {
+    __bf16* tw;
+    hipMalloc(&tw, (size_t)M * 2 * N * 2 * 3);
+    a.p[0].outh = tw;
+    a.p[0].hps = (long long)M * 2 * N;
+    a.p[0].hnp = 3;
+    printf("K64 bias+elu+store+3 planes  %.2f us\n", time_it(a, 1, 200));
+    phases("K64 twin", 8 * g_rb);
+    a.p[0].out = nullptr;
+    printf("K64 bias+elu+3 planes only   %.2f us\n", time_it(a, 1, 200));
+    a.p[0] = p;
+    hipFree(tw);
+  }
   a.p[0].act = 0;
   printf("K64 bias+store (no elu)      %.2f us\n", time_it(a, 1, 200));
   a.p[0].out = nullptr;
   printf("K64 no store                 %.2f us\n", time_it(a, 1, 200));
-  phases("K64 nostore", 8 * 128);
+  phases("K64 nostore", 8 * g_rb);
   a.p[0] = p;
   a.p[0].K = 8;
   a.p[0].ldx = 8;
   printf("K8 bias+elu+store            %.2f us\n", time_it(a, 1, 200));
-  phases("K8", 8 * 128);
+  phases("K8", 8 * g_rb);
   a.p[0] = p;
   a.p[1] = p;
   a.p[1].out = out + N;
