@@ -341,7 +341,7 @@ def main():
                              for k, v in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])},
     }
     hbm = {}
-    for key in ("adam", "soft_update", "gather"):
+    for key in ("adam+soft_update", "adam", "soft_update", "gather"):
         if key in by_kernel and by_kernel[key]["ms"] > 0:
             k = by_kernel[key]
             hbm[key] = round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1)

@@ -906,9 +906,10 @@ static void stats_allreduce(ddpg_ctx* c) {
 }
 
 // TF ApplyAdam over one network's flat region.  advance: also advance its
-// beta powers right after (1:1 API path); the fused step advances both in
-// the soft-update kernel instead.
-static void adam_launch(ddpg_ctx* c, int net, bool advance) {
+// beta powers right after (1:1 API path).  soft (fused step): the same pass
+// also soft-updates this network's targets from the new parameters; the
+// fused step then advances both networks' beta powers at its end.
+static void adam_launch(ddpg_ctx* c, int net, bool advance, bool soft = false) {
   const size_t b = net == 0 ? c->L.actor_begin : c->L.critic_begin;
   const size_t e = net == 0 ? c->L.actor_end : c->L.critic_end;
   const long long n = (long long)(e - b);
@@ -916,13 +917,15 @@ static void adam_launch(ddpg_ctx* c, int net, bool advance) {
   int blocks = (int)std::min<long long>(4096, std::max<long long>(1, (n / 4 + 255) / 256));
   c->sb_shadow_ok = false;
   {
-    ProfScope ps(c, "adam", 0, 28.0 * n);
-    // keeps theta's twin current, or leaves it stale if it already was
+    const float tau = c->cfg.tau, omt = (float)(1.0 - (double)tau);
+    ProfScope ps(c, soft ? "adam+soft_update" : "adam", 0, (soft ? 40.0 : 28.0) * n);
+    // keeps theta's (and theta''s) twin current, or leaves it stale if it already was
     __bf16* tw = (c->hnp && c->wtw_ok) ? c->wtw + b : nullptr;
+    __bf16* ttw = (c->hnp && c->wtw_ok) ? c->wtw + (size_t)c->hnp * c->L.total + b : nullptr;
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
                        c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net, lr,
                        c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon, tw, (long long)c->L.total,
-                       c->hnp);
+                       c->hnp, soft ? c->target + b : nullptr, tau, omt, soft ? ttw : nullptr);
     HIP_TRY(hipGetLastError());
   }
   if (advance) {
@@ -1043,7 +1046,7 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.critic_begin, L.critic_end - L.critic_begin);
   stats_allreduce(c);
-  adam_launch(c, 1, !fused);
+  adam_launch(c, 1, !fused, fused);
 }
 
 // Actor update given dz3 (= TanhGrad chain of -dQ/da) and the forward
@@ -1149,7 +1152,7 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   add_wgrad(tab, pW3, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A);
   reduce_launch(c, "grad_reduce", tab);
   allreduce(c, G + L.actor_begin, L.actor_end - L.actor_begin);
-  adam_launch(c, 0, !fused);
+  adam_launch(c, 0, !fused, fused);
 }
 
 // Soft target update (networks.py:34-37) over the selected networks; pw_mask
@@ -1220,8 +1223,11 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);
   // actor.train(s, grads[0])  ddpg.py:109  (forward above reused: same params)
   actor_train_dev(c, B, true, c->par);
-  // actor/critic.update_target_network()  ddpg.py:112-113 (+ both Adam power updates)
-  soft_update_dev(c, DDPG_SOFT_ACTOR | DDPG_SOFT_CRITIC, 3);
+  // actor/critic.update_target_network()  ddpg.py:112-113: done inside each
+  // network's Adam pass above; here both Adam power updates (_finish)
+  hipLaunchKernelGGL(advance_powers_kernel, dim3(1), dim3(1), 0, c->cur, c->dpw, 3,
+                     c->cfg.beta1, c->cfg.beta2);
+  HIP_TRY(hipGetLastError());
 }
 
 // Rebuild the W^T shadows of the small path after a parameter write outside

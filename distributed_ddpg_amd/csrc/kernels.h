@@ -388,10 +388,16 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceTable tab) {
 // advances them (b1p *= b1, b2p *= b2), i.e. the AdamOptimizer._finish update.
 // tw (optional): the bf16 twin of p (tnp planes, tps elements apart), kept
 // current for the bf16-operand GEMMs.
+// tt (optional, fused learner step): the network's target parameters, soft-
+// updated from the new p in the same pass (networks.py:34-37, the same fp32
+// ops as soft_update_kernel; nothing reads the targets between this network's
+// Adam step and the end of the step), ttw its twin.
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ g, long long n,
                             const float* __restrict__ pw, float lr, float b1, float b2,
-                            float eps, __bf16* __restrict__ tw, long long tps, int tnp) {
+                            float eps, __bf16* __restrict__ tw, long long tps, int tnp,
+                            float* __restrict__ tt, float tau, float omt,
+                            __bf16* __restrict__ ttw) {
   const float b1p = pw[0], b2p = pw[1];
   const float alpha = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.f, b2p))),
                                 __fsub_rn(1.f, b1p));
@@ -418,6 +424,15 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
     reinterpret_cast<float4*>(m)[i] = Mv;
     reinterpret_cast<float4*>(v)[i] = V;
     if (tw) store_twin4(tw + 4 * i, tps, tnp, P);
+    if (tt) {
+      float4 b = reinterpret_cast<float4*>(tt)[i];
+      b.x = __fadd_rn(__fmul_rn(P.x, tau), __fmul_rn(b.x, omt));
+      b.y = __fadd_rn(__fmul_rn(P.y, tau), __fmul_rn(b.y, omt));
+      b.z = __fadd_rn(__fmul_rn(P.z, tau), __fmul_rn(b.z, omt));
+      b.w = __fadd_rn(__fmul_rn(P.w, tau), __fmul_rn(b.w, omt));
+      reinterpret_cast<float4*>(tt)[i] = b;
+      if (ttw) store_twin4(ttw + 4 * i, tps, tnp, b);
+    }
   }
   // tail (n % 4)
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
@@ -426,6 +441,10 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
     v[i] = __fadd_rn(v[i], __fmul_rn(__fsub_rn(__fmul_rn(g[i], g[i]), v[i]), omb2));
     p[i] = __fsub_rn(p[i], __fdiv_rn(__fmul_rn(m[i], alpha), __fadd_rn(__fsqrt_rn(v[i]), eps)));
     if (tw) store_twin1(tw + i, tps, tnp, p[i]);
+    if (tt) {
+      tt[i] = __fadd_rn(__fmul_rn(p[i], tau), __fmul_rn(tt[i], omt));
+      if (ttw) store_twin1(ttw + i, tps, tnp, tt[i]);
+    }
   }
 }
 
