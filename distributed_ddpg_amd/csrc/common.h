@@ -60,6 +60,25 @@ DDPG_DEV void store_twin4(__bf16* q, long long ps, int np, float4 v) {
     *reinterpret_cast<bf16x4*>(q) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
   }
 }
+// Twin of 8 consecutive fp32 values (a, b): one 16-B store per plane (q and
+// ps multiples of 8 elements).
+DDPG_DEV void store_twin8(__bf16* q, long long ps, int np, float4 a, float4 b) {
+  bf16x2 h[4], m[4], l[4];
+  const f32x2v x[4] = {f32x2v{a.x, a.y}, f32x2v{a.z, a.w}, f32x2v{b.x, b.y}, f32x2v{b.z, b.w}};
+  if (np == 3) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split3_pair(x[i], h[i], m[i], l[i]);
+    *reinterpret_cast<bf16x8*>(q + ps) =
+        bf16x8{m[0][0], m[0][1], m[1][0], m[1][1], m[2][0], m[2][1], m[3][0], m[3][1]};
+    *reinterpret_cast<bf16x8*>(q + 2 * ps) =
+        bf16x8{l[0][0], l[0][1], l[1][0], l[1][1], l[2][0], l[2][1], l[3][0], l[3][1]};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = __builtin_convertvector(x[i], bf16x2);
+  }
+  *reinterpret_cast<bf16x8*>(q) =
+      bf16x8{h[0][0], h[0][1], h[1][0], h[1][1], h[2][0], h[2][1], h[3][0], h[3][1]};
+}
 DDPG_DEV void store_twin1(__bf16* q, long long ps, int np, float x) {
   const __bf16 h = (__bf16)x;
   q[0] = h;

@@ -238,6 +238,12 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   const bool vst = outp && ((N | e.ldo) & 3) == 0 && (e.out_split_stride & 3) == 0 &&
                    ((uintptr_t)outp & 15) == 0;
   constexpr int C4 = BN / 4, RPR = NT / C4;  // float4 columns per row, rows per round
+  // 8-column rows (16-B twin stores) when every row start is 16-B aligned
+  const bool oct = (N & 7) == 0 && (!outp || (vst && (e.ldo & 7) == 0)) &&
+                   (!e.outh || ((e.ldo & 7) == 0 && (e.h_plane_stride & 7) == 0 &&
+                                (e.out_split_stride & 7) == 0 &&
+                                ((uintptr_t)e.outh & 15) == 0)) &&
+                   BN % 8 == 0 && NT % (BN / 8) == 0;
   constexpr int CG = NT / BN;  // column-sum row groups
   float csum = 0.f;
 #pragma unroll
@@ -254,7 +260,28 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           }
     }
     __syncthreads();
-    if (outp || e.outh) {
+    if ((outp || e.outh) && oct) {
+      // 8 columns per thread: 16-B stores for the fp32 rows and every twin plane
+      constexpr int C8 = BN / 8, RPR8 = NT / C8;
+      const int c8 = tid % C8, rr0 = tid / C8, n = n0 + 8 * c8;
+      if (n < N) {
+#pragma unroll 2
+        for (int rr = rr0; rr < WR; rr += RPR8) {
+          const int m = m0 + pass * WR + rr;
+          if (m >= M) continue;
+          const float4 va = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 8 * c8);
+          const float4 vb = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 8 * c8 + 4);
+          const size_t o = (size_t)m * e.ldo + n;
+          if (e.outh)
+            store_twin8(e.outh + (size_t)z * e.out_split_stride + o, e.h_plane_stride,
+                        e.h_planes, va, vb);
+          if (outp) {
+            *reinterpret_cast<float4*>(outp + o) = va;
+            *reinterpret_cast<float4*>(outp + o + 4) = vb;
+          }
+        }
+      }
+    } else if (outp || e.outh) {
       const int c4 = tid % C4, rr0 = tid / C4, n = n0 + 4 * c4;
 #pragma unroll 4
       for (int rr = rr0; rr < WR; rr += RPR) {
