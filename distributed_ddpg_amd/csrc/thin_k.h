@@ -6,16 +6,15 @@
 // kernel is LDS-bandwidth-bound (every fmaf operand pair comes from LDS).
 //
 // Here a workgroup (4 waves) owns a 64-row x 128-column output block.  The
-// K x 128 weight panel is staged once in LDS; each wave owns 32 rows x 64
-// columns (two 32x32 fp32 MFMA tiles, v_mfma_f32_32x32x2_f32: exact fp32
-// products, fp32 accumulation) and feeds its A operand straight from global
-// memory: lane l holds row l&31 and the k half (l>>5) -- the MFMA's two k
-// slots walk k = h*K/2 + j, j = 0 .. K/2-1, so each lane's X operands are
-// K/2 consecutive floats (float4 loads).  The fused epilogue has the
-// gemm_common.h semantics (bias, elu, EluGrad multiply, bias-gradient column
-// sums).  Two independent layers writing different column ranges of one
-// output (the critic's [state | action] concat) share one launch (blockIdx.z
-// selects the part).
+// K x 128 weight panel and the 64 x K input tile are split once into their
+// exact three bf16 planes (x = h + m + l) in LDS; each wave owns 32 rows x 64
+// columns (two 32x32 tiles) and takes the six plane products of the twin GEMM
+// (gemm_h.h) per 16-deep step on v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation -- 2.7x the fp32-input MFMA rate at the same accuracy class as
+// the large GEMMs.  The fused epilogue has the gemm_common.h semantics (bias,
+// elu, EluGrad multiply, bias-gradient column sums).  Two independent layers
+// writing different column ranges of one output (the critic's [state |
+// action] concat) share one launch (blockIdx.z selects the part).
 #pragma once
 #include "common.h"
 
@@ -54,21 +53,30 @@ struct TkArgs {
   int M;
 };
 
-typedef float tk_f32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) tk_f32x2 tk_lds_v2;
-
-
 constexpr int TK_VLD = TK_COLS + 4;  // LDS row stride of the output tile (floats)
-constexpr int TK_SMEM =
-    TK_MAXK * TK_COLS > TK_ROWS * TK_VLD ? TK_MAXK * TK_COLS : TK_ROWS * TK_VLD;
+
+// Three-plane bf16 images in LDS (the exact split x = h + m + l of every fp32
+// operand, as the twins of gemm_h.h): [plane][row][64 k] with 128-B rows,
+// 16-B chunk c of row r at c ^ ((r >> 1) & 7) -- every 32x32x16 fragment read
+// (lane: row l & 31, chunk 2 ks + (l >> 5)) is bank-conflict-free.  X rows are
+// batch rows; W rows are output columns (W^T), so both operands are read the
+// same way.
+constexpr int TK_XIMG = TK_ROWS * 128;  // bytes per X plane
+constexpr int TK_WIMG = TK_COLS * 128;  // bytes per W plane
+constexpr int TK_OUT_BYTES = TK_ROWS * TK_VLD * 4;
+constexpr int TK_WREG = 3 * TK_WIMG > TK_OUT_BYTES ? 3 * TK_WIMG : TK_OUT_BYTES;
+constexpr int TK_LDS = TK_WREG + 3 * TK_XIMG;
+DDPG_DEV int tk_swz(int r) { return (r >> 1) & 7; }
+DDPG_DEV int tk_off(int r, int k) { return r * 128 + 16 * ((k >> 3) ^ tk_swz(r)) + 2 * (k & 7); }
 
 __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
-  // W panel as [k][wave column half][col 0..31][tile 0..1]: one ds_read_b64
-  // per MFMA step gives a lane both of its B operands; after the MFMAs the
-  // same LDS holds the raw output tile [64 rows][TK_VLD]
-  __shared__ __attribute__((aligned(16))) float Ws[TK_SMEM];
-  __shared__ float red[8 * TK_COLS];
-  __shared__ __attribute__((aligned(16))) float Xs[TK_ROWS * (TK_MAXK + 4)];
+  // W image (3 planes), after the MFMAs the raw output tile [64 rows][TK_VLD];
+  // then the X image (3 planes)
+  __shared__ __attribute__((aligned(16))) char lds[TK_LDS];
+  __shared__ float red[16 * TK_COLS];
+  float* const Ws = reinterpret_cast<float*>(lds);
+  char* const wimg = lds;
+  char* const ximg = lds + TK_WREG;
   const TkPart P = blockIdx.z ? args.p[1] : args.p[0];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, h = lane >> 5;
@@ -76,94 +84,93 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   const int m0 = blockIdx.y * TK_ROWS, n0 = blockIdx.x * TK_COLS;
   if (n0 >= P.N) return;
   TK_STAMP(0);
-  const int K = P.K, M = args.M, K4 = K >> 2, KH = K >> 1, K8 = K >> 3;
-  // ---- global loads: W panel (<= 8 float4 per thread) and this lane's X row
-  f32x4 wv[8], xv[8];
-  if (!P.w_nk) {  // W[k][n]: float4 of 4 columns, rows k = (tid >> 5) + 8 j
-    const int c4 = tid & 31, kr = tid >> 5, n = n0 + 4 * c4;
+  const int K = P.K, M = args.M;
+  const int KS = (K + 15) >> 4;  // 16-deep MFMA steps; k in [K, 16 KS) are zeros
+  const int KP = 16 * KS;
+  // ---- global loads: thread (column c, k quads kq + 2 j) of the W panel, and
+  // 4 float4 quads of the X tile (64 rows x 16 quads)
+  const int wcol = tid & 127, kq = tid >> 7, wn = n0 + wcol;
+  f32x4 wv[8], xg[4];
+  {
+    const bool wvec = P.w_nk && ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = kr + 8 * j;
+      const int k = 4 * (kq + 2 * j);
       wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (k < K && n < P.N) wv[j] = *reinterpret_cast<const f32x4*>(P.W + (size_t)k * P.ldw + n);
-    }
-  } else {  // W[n][k]: 4 k per load, column c = tid & 127, k quads (tid >> 7) + 2 j
-    // (rows of an unaligned stride, e.g. W3 [H2][A = 17], load as scalars)
-    const int c = tid & 127, kq = tid >> 7, n = n0 + c;
-    const bool wvec = ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
+      if (k < K && wn < P.N) {
+        if (P.w_nk) {  // W[n][k]: 4 consecutive k (rows of an unaligned stride as scalars)
+          const float* q = P.W + (size_t)wn * P.ldw + k;
+          wv[j] = wvec ? *reinterpret_cast<const f32x4*>(q) : f32x4{q[0], q[1], q[2], q[3]};
+        } else {  // W[k][n]: 4 rows of column n (each load coalesced over the 128 columns)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k4 = kq + 2 * j;
-      wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (k4 < K4 && n < P.N) {
-        const float* q = P.W + (size_t)n * P.ldw + 4 * k4;
-        wv[j] = wvec ? *reinterpret_cast<const f32x4*>(q) : f32x4{q[0], q[1], q[2], q[3]};
+          for (int e = 0; e < 4; ++e) wv[j][e] = P.W[(size_t)(k + e) * P.ldw + wn];
+        }
       }
     }
   }
-  // X tile [64 rows][K] -> LDS with coalesced float4 loads (a lane's own row
-  // would otherwise be 8 loads touching 64 different rows per instruction)
-  const int XLD = K + 4;  // padded row stride: conflict-free ds_read_b128 below
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int f = tid + TK_NT * j, r = f / K4, k4 = f - r * K4, m = m0 + r;
-    if (r < TK_ROWS) {
-      f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (m < M) x = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + 4 * k4);
-      *reinterpret_cast<f32x4*>(Xs + r * XLD + 4 * k4) = x;
-    }
+    const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15), m = m0 + r;
+    xg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (k < K && m < M) xg[j] = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + k);
   }
-  // ---- W panel -> LDS: column nl -> (half nl >> 6, tile (nl >> 5) & 1, col nl & 31)
-  auto ws_at = [](int k, int nl) { return ((k * 2 + (nl >> 6)) * 32 + (nl & 31)) * 2 + ((nl >> 5) & 1); };
-  if (!P.w_nk) {
-    const int c4 = tid & 31, kr = tid >> 5;
+  // ---- split into the plane images
+  auto put4 = [&](char* img, int plane_bytes, int r, int k, f32x4 v) {
+    bf16x2 h0, m0_, l0, h1, m1, l1;
+    split3_pair(f32x2v{v[0], v[1]}, h0, m0_, l0);
+    split3_pair(f32x2v{v[2], v[3]}, h1, m1, l1);
+    const int off = tk_off(r, k);
+    *reinterpret_cast<bf16x4*>(img + off) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+    *reinterpret_cast<bf16x4*>(img + plane_bytes + off) = bf16x4{m0_[0], m0_[1], m1[0], m1[1]};
+    *reinterpret_cast<bf16x4*>(img + 2 * plane_bytes + off) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+  };
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = kr + 8 * j;
-      if (k < K) {
+  for (int j = 0; j < 8; ++j) {
+    const int k = 4 * (kq + 2 * j);
+    if (k < KP) put4(wimg, TK_WIMG, wcol, k, wv[j]);
+  }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Ws[ws_at(k, 4 * c4 + e)] = wv[j][e];
-      }
-    }
-  } else {
-    const int c = tid & 127, kq = tid >> 7;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k4 = kq + 2 * j;
-      if (k4 < K4) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Ws[ws_at(4 * k4 + e, c)] = wv[j][e];
-      }
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15);
+    if (k < KP) put4(ximg, TK_XIMG, r, k, xg[j]);
   }
   __syncthreads();
-  {
-    const float* xr = Xs + (32 * wr + li) * XLD + h * KH;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      xv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (q < K8) xv[q] = *reinterpret_cast<const f32x4*>(xr + 4 * q);
-    }
-  }
   TK_STAMP(1);
-  // ---- MFMA: step j contracts k = j (lanes 0-31) and k = KH + j (lanes 32-63)
-  f32x16 acc[2];
+  // ---- MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulation): per 16-deep step
+  // the six plane products hh, hm, mh, hl, lh, mm of gemm_h.h, the five small
+  // ones in their own accumulator.  Wave (wr, wc): rows 32 wr + li, columns
+  // 64 wc + 32 t + li (t = 0, 1).
+  f32x16 acc[2], acs[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  const tk_lds_v2* Wb = reinterpret_cast<const tk_lds_v2*>(LDS(Ws)) + (h * KH * 2 + wc) * 32 + li;
+    for (int r = 0; r < 16; ++r) acc[t][r] = acs[t][r] = 0.f;
+  const int ra = 32 * wr + li;
+  for (int ks = 0; ks < KS; ++ks) {
+    const int kk = 16 * ks + 8 * h;
+    bf16x8 a[3], b[2][3];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    if (q < K8) {
+    for (int p = 0; p < 3; ++p) {
+      a[p] = *reinterpret_cast<const bf16x8*>(ximg + p * TK_XIMG + tk_off(ra, kk));
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const tk_f32x2 b = Wb[(4 * q + jj) * 64];
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[q][jj], b[0], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[q][jj], b[1], acc[1], 0, 0, 0);
-      }
+      for (int t = 0; t < 2; ++t)
+        b[t][p] = *reinterpret_cast<const bf16x8*>(wimg + p * TK_WIMG +
+                                                   tk_off(64 * wc + 32 * t + li, kk));
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 q = acs[t];
+      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[t][0], q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][1], q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][2], q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][0], q, 0, 0, 0);
+      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][1], q, 0, 0, 0);
+      acs[t] = q;
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][0], acc[t], 0, 0, 0);
     }
   }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) acc[t] += acs[t];
   TK_STAMP(2);
   // ---- epilogue.  The raw tile goes through LDS (lane li of tile t holds
   // column li, register r row (r & 3) + 8 (r >> 2) + 4 h) so that every
@@ -180,47 +187,74 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   }
   __syncthreads();
   TK_STAMP(3);
-  // thread -> column quad c4 = tid & 31, rows rg, rg + 8, ... (rg = tid >> 5)
-  const int c4 = tid & 31, rg = tid >> 5, n = n0 + 4 * c4;
-  const bool nok = n < P.N;  // N % 4 == 0: a quad is all in or all out
-  f32x4 bq = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (P.bias && nok) bq = *reinterpret_cast<const f32x4*>(P.bias + n);
-  f32x4 csum = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int RPT = TK_ROWS / 8;  // rows per thread
-  f32x4 aq[RPT];
+  // thread -> column octet c8 = tid & 15, rows rg + 16 i (rg = tid >> 4):
+  // 16-B fp32 and twin-plane stores
+  const int c8 = tid & 15, rg = tid >> 4, n = n0 + 8 * c8;
+  const bool q0 = n < P.N, q1 = n + 4 < P.N;  // N % 4 == 0: quads all in or all out
+  const bool oct = q1 && ((P.ldo & 7) == 0) && ((P.hps & 7) == 0) &&
+                   (((uintptr_t)P.outh & 15) == 0);
+  f32x4 bq0 = f32x4{0.f, 0.f, 0.f, 0.f}, bq1 = bq0;
+  if (P.bias && q0) bq0 = *reinterpret_cast<const f32x4*>(P.bias + n);
+  if (P.bias && q1) bq1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
+  float csum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  constexpr int RPT = TK_ROWS / 16;  // rows per thread
+  f32x4 aq[RPT][2];
   if (P.aux) {  // all aux loads in flight before the first use
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const int m = m0 + rg + 8 * i;
-      aq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (nok && m < M) aq[i] = *reinterpret_cast<const f32x4*>(P.aux + (size_t)m * P.ldaux + n);
+      const int m = m0 + rg + 16 * i;
+      aq[i][0] = aq[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < M) {
+        const float* ap = P.aux + (size_t)m * P.ldaux + n;
+        if (q0) aq[i][0] = *reinterpret_cast<const f32x4*>(ap);
+        if (q1) aq[i][1] = *reinterpret_cast<const f32x4*>(ap + 4);
+      }
     }
   }
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int rl = rg + 8 * i, m = m0 + rl;
-    if (!nok || m >= M) continue;
-    f32x4 v = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 4 * c4);
+    const int rl = rg + 16 * i, m = m0 + rl;
+    if (!q0 || m >= M) continue;
+    f32x4 v[2];
+    v[0] = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 8 * c8);
+    v[1] = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 8 * c8 + 4);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x = v[e];
-      if (P.bias) x = __fadd_rn(x, bq[e]);
-      if (P.act == 1) x = elu_f(x);
-      if (P.aux) x = __fmul_rn(x, elu_grad_factor(aq[i][e]));
-      v[e] = x;
-      csum[e] += x;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = v[u][e];
+        if (P.bias) x = __fadd_rn(x, u ? bq1[e] : bq0[e]);
+        if (P.act == 1) x = elu_f(x);
+        if (P.aux) x = __fmul_rn(x, elu_grad_factor(aq[i][u][e]));
+        v[u][e] = x;
+        if (u == 0 || q1) csum[4 * u + e] += x;
+      }
+    const size_t o = (size_t)m * P.ldo + n;
+    const float4 va = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]);
+    const float4 vb = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
+    if (P.out) {
+      *reinterpret_cast<f32x4*>(P.out + o) = v[0];
+      if (q1) *reinterpret_cast<f32x4*>(P.out + o + 4) = v[1];
     }
-    if (P.out) *reinterpret_cast<f32x4*>(P.out + (size_t)m * P.ldo + n) = v;
-    if (P.outh) store_twin4(P.outh + (size_t)m * P.ldo + n, P.hps, P.hnp, make_float4(v[0], v[1], v[2], v[3]));
+    if (P.outh) {
+      if (oct) {
+        store_twin8(P.outh + o, P.hps, P.hnp, va, vb);
+      } else {
+        store_twin4(P.outh + o, P.hps, P.hnp, va);
+        if (q1) store_twin4(P.outh + o + 4, P.hps, P.hnp, vb);
+      }
+    }
   }
   if (P.colsum) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[rg * TK_COLS + 4 * c4 + e] = csum[e];
+    for (int e = 0; e < 8; ++e) red[rg * TK_COLS + 8 * c8 + e] = csum[e];
     __syncthreads();
     if (tid < TK_COLS && n0 + tid < P.N) {
       float s = 0.f;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) s += red[g * TK_COLS + tid];
+      for (int g = 0; g < 16; ++g) s += red[g * TK_COLS + tid];
       P.colsum[(size_t)blockIdx.y * P.ld_colsum + n0 + tid] = s;
     }
   }
