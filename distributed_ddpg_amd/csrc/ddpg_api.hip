@@ -435,6 +435,36 @@ static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const Ge
     hipLaunchKernelGGL((gemm_f32_kernel<AL, BL, VA, VB, 64, 64>), grid, dim3(GNT), 0, st, g);
 }
 
+// XCD tile order for an nx x ny grid of BM x BN tiles (xcd_tile): the
+// rectangle of tiles per XCD with the fewest operand-panel bytes
+// (H row panels of BM rows + W column panels of BN columns), when 8 such
+// rectangles tile the grid and it reads fewer bytes than the row-major runs.  env DDPG_XCD_RECT=0
+// keeps the runs.
+static int g_xcd_rect = -1;
+static int xcd_rect(int on, int nx, int ny, int BM, int BN) {
+  if (g_xcd_rect < 0) {
+    const char* v = getenv("DDPG_XCD_RECT");
+    g_xcd_rect = !(v && atoi(v) == 0);
+  }
+  if (!on || !g_xcd_rect || (nx * ny) % 8) return on;
+  const int T = nx * ny / 8;
+  int best = -1, best_cost = 0;
+  for (int W = 1; W <= nx; ++W) {
+    if (nx % W || T % W) continue;
+    const int H = T / W;
+    if (ny % H || (nx / W) * (ny / H) != 8) continue;
+    const int cost = H * BM + W * BN;
+    if (best < 0 || cost < best_cost) {
+      best = W;
+      best_cost = cost;
+    }
+  }
+  // keep the row-major runs unless the rectangle reads strictly fewer bytes
+  const int run_cost = T % nx ? -1 : (T / nx) * BM + nx * BN;
+  if (best < 0 || (run_cost >= 0 && best_cost >= run_cost)) return on;
+  return 16 + best;
+}
+
 static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec);
 static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec);
 
@@ -530,7 +560,7 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       a.lda = lda;
       a.ldb = ldb;
       a.kps = h.kps;
-      a.xcd = g_xcd_remap;
+      a.xcd = xcd_rect(g_xcd_remap, h.nt(N), h.mt(M), BMh, HG_BN);
       a.e = ee;
       static const char* lay[2] = {"RK", "KR"};
       // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)

@@ -83,10 +83,23 @@ struct GemmArgs {
 // L2s.  Remap so each XCD owns a contiguous run of row-major tiles (whole
 // rows of m-tiles share their A panel in one L2).  Speed only; any placement
 // is correct.
+// on >= 16: each XCD owns a W x H rectangle of tiles (W = on - 16 columns,
+// H = tiles per XCD / W rows; the host checks that 8 rectangles tile the
+// grid), so it reads H row panels of A and W column panels of B instead of
+// the whole B panel.
 DDPG_DEV void xcd_tile(int& bx, int& by, int on) {
   if (!on) {
     bx = blockIdx.x;
     by = blockIdx.y;
+    return;
+  }
+  if (on >= 16) {
+    const int W = on - 16, nx = gridDim.x;
+    const int lin = blockIdx.x + blockIdx.y * nx;
+    const int x = lin & 7, idx = lin >> 3;
+    const int H = ((nx * gridDim.y) >> 3) / W, rx = nx / W;
+    bx = (x % rx) * W + idx % W;
+    by = (x / rx) * H + idx / W;
     return;
   }
   const int nx = gridDim.x;
