@@ -462,14 +462,24 @@ def test_small_batch_path_matches_large_path(dd, O, monkeypatch, name):
     from distributed_ddpg_amd import _lib
     from distributed_ddpg_amd.learner import FusedLearner, Profile
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    import random
     S, A, H1, H2, scale, B, _ = CONFIGS[name]
     p, _ = _params(O, name)
+    # the oracle on the same rows (the replay's sampler = random.Random(5))
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    L32 = O.Learner(S, A, H1, H2, scale, dtype=np.float32, params=p, init_blend=False)
+    ref_rng = random.Random(5)
     res = {}
     for small in ("1", "0"):
         monkeypatch.setenv("DDPG_SMALL", small)
         sess, actor, critic = _session(dd, O, name, p)
         rb = ReplayBuffer(4000, 5)
-        _fill(rb, S, A, 3000, scale, seed=8)
+        rows = _fill(rb, S, A, 3000, scale, seed=8)
+        if small == "1":
+            for _ in range(4):
+                idx = np.array(ref_rng.sample(range(3000), B))
+                L.step(*(x[idx] for x in rows))
+                L32.step(*(x[idx] for x in rows))
         fl = FusedLearner(sess, rb, B)
         prof = Profile(sess)
         prof.enable(True)
@@ -489,6 +499,13 @@ def test_small_batch_path_matches_large_path(dd, O, monkeypatch, name):
     for x, y in zip(p1, p0):
         for u, v in zip(x, y):
             assert rel(u, v) < GRAD_TOL
+    # and each path against the oracle
+    nets = (("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS), ("actor_t", O.ACTOR_KEYS),
+            ("critic_t", O.CRITIC_KEYS))
+    for params in (p1, p0):
+        for (net, keys), vals in zip(nets, params):
+            for k, v in zip(keys, vals):
+                assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (net, k))
 
 
 @pytest.mark.parametrize("name", ["ip", "odd"])
