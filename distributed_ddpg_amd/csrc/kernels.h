@@ -240,10 +240,28 @@ __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
   float4 sw = make_float4(0.f, 0.f, 0.f, 0.f), sb = sw;
   if (j < H2) {
     const float4 w = *reinterpret_cast<const float4*>(Wo + j);
-#pragma unroll 4
-    for (int b = b0 + rg; b < b1; b += 4) {
-      const float4 hv = *reinterpret_cast<const float4*>(h + (size_t)b * ldh + j);
-      const float d = dq[b];
+    // 16 rows per batch, all loads in flight before the first use (one HBM
+    // round trip per batch instead of one per 4 rows)
+    constexpr int RB = 16;
+    for (int bb = b0 + rg; bb < b1; bb += 4 * RB) {
+    float4 hvs[RB];
+    float ds[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int b = bb + 4 * i;
+      hvs[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      ds[i] = 0.f;
+      if (b < b1) {
+        hvs[i] = *reinterpret_cast<const float4*>(h + (size_t)b * ldh + j);
+        ds[i] = dq[b];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int b = bb + 4 * i;
+      if (b >= b1) continue;
+      const float4 hv = hvs[i];
+      const float d = ds[i];
       float4 dp;
       dp.x = __fmul_rn(__fmul_rn(d, w.x), elu_grad_factor(hv.x));
       dp.y = __fmul_rn(__fmul_rn(d, w.y), elu_grad_factor(hv.y));
@@ -259,6 +277,7 @@ __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
       sb.y += dp.y;
       sb.z += dp.z;
       sb.w += dp.w;
+    }
     }
   }
   if (rg > 0) {
