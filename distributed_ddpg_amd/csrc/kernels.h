@@ -29,8 +29,30 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  // fp32 ring with 4-aligned rows: 16-B accesses (4 features per lane)
+  const bool v4 = !rsd && (S & 3) == 0 && (lds & 3) == 0 && (hps & 3) == 0;
   for (int b = wave; b < B; b += nwaves) {
     const size_t slot = (size_t)slots[b];
+    if (v4) {
+      for (int j = 4 * lane; j < S; j += 256) {
+        const size_t e = slot * S + j;
+        float4 x = *reinterpret_cast<const float4*>(rs + e);
+        float4 x2 = *reinterpret_cast<const float4*>(rs2 + e);
+        if (mean) {
+          float* px = &x.x;
+          float* px2 = &x2.x;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            px[q] = (float)(((double)px[q] - mean[j + q]) / scale[j + q]);
+            px2[q] = (float)(((double)px2[q] - mean[j + q]) / scale[j + q]);
+          }
+        }
+        *reinterpret_cast<float4*>(s + (size_t)b * lds + j) = x;
+        *reinterpret_cast<float4*>(s2 + (size_t)b * lds + j) = x2;
+        if (sh) store_twin4(sh + (size_t)b * lds + j, hps, hnp, x);
+        if (s2h) store_twin4(s2h + (size_t)b * lds + j, hps, hnp, x2);
+      }
+    } else
     for (int j = lane; j < S; j += 64) {
       const size_t e = slot * S + j;
       float x, x2;
