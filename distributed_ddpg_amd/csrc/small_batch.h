@@ -371,29 +371,6 @@ DDPG_DEV void sb_alpha_and_advance(float* pw, float* alpha, float lr, float b1, 
   pw[1] = __fmul_rn(b2p, b2);
 }
 
-// dst[k][r] = ring[slot(r0 + r)][k] for k < cols, zero up to ldk features and
-// for rows past `valid`; read from the float64 plane `ringd` when the ring
-// keeps one; the scaler (x - mean) / scale in fp64 when mean, then one
-// rounding to fp32 (the reference's preprocess_input + feed_dict cast).
-// save (optional): the valid rows also go to save[k * Bp + r0 + r].
-DDPG_DEV void sb_gather(lds_f* dst, int ldk, const float* __restrict__ ring,
-                        const double* __restrict__ ringd, int cols,
-                        const int* __restrict__ slots, int r0, int valid,
-                        const double* __restrict__ mean, const double* __restrict__ sdev,
-                        float* __restrict__ save, int Bp) {
-  for (int idx = threadIdx.x; idx < 4 * ldk; idx += SB_NT) {
-    const int k = idx >> 2, r = idx & 3;
-    float x = 0.f;
-    if (r < valid && k < cols) {
-      const size_t e = (size_t)slots[r0 + r] * cols + k;
-      const double xd = ringd ? ringd[e] : (double)ring[e];
-      x = mean ? (float)((xd - mean[k]) / sdev[k]) : (float)xd;
-      if (save) save[(size_t)k * Bp + r0 + r] = x;
-    }
-    dst[idx] = x;
-  }
-}
-
 // save[k][r0 .. r0 + 3] = src[k][0 .. 3] (feature-major, one float4 per
 // feature; rows past B land in the padding that no reader sums).
 DDPG_DEV void sb_save(float* __restrict__ save, int Bp, int cols, const lds_f* src, int r0) {
@@ -426,9 +403,34 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   SB_STAMP(0);
 
   if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw + 2, g.alpha + 1, g.lr_c, g.b1, g.b2);
-  sb_gather(xs, LX, g.rs, g.rsd, g.S, g.slots, r0, valid, g.mean, g.sdev, g.sv.xs, g.sv.Bp);
-  sb_gather(xs2, LX, g.rs2, g.rs2d, g.S, g.slots, r0, valid, g.mean, g.sdev, nullptr, 0);
-  sb_gather(xa, LX, g.ra, nullptr, g.A, g.slots, r0, valid, nullptr, nullptr, g.sv.xa, g.sv.Bp);
+  // rows -> xs / xs2 / xa ([feature][4], zero past S / A and for rows past
+  // `valid`) in one pass: one slot read, then every ring read of an element in
+  // flight together; from the float64 ring planes when the ring keeps them; the
+  // scaler (x - mean) / scale in fp64 before the one rounding to fp32 (the
+  // reference's preprocess_input + feed_dict cast); xs / xa also saved
+  // feature-major for the weight gradients
+  for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
+    const int k = idx >> 2, r = idx & 3;
+    float x = 0.f, x2 = 0.f, xv = 0.f;
+    if (r < valid) {
+      const size_t sl = (size_t)g.slots[r0 + r];
+      if (k < g.S) {
+        const size_t e = sl * g.S + k;
+        const double xd = g.rsd ? g.rsd[e] : (double)g.rs[e];
+        const double x2d = g.rs2d ? g.rs2d[e] : (double)g.rs2[e];
+        x = g.mean ? (float)((xd - g.mean[k]) / g.sdev[k]) : (float)xd;
+        x2 = g.mean ? (float)((x2d - g.mean[k]) / g.sdev[k]) : (float)x2d;
+        g.sv.xs[(size_t)k * g.sv.Bp + r0 + r] = x;
+      }
+      if (k < g.A) {
+        xv = g.ra[sl * g.A + k];
+        g.sv.xa[(size_t)k * g.sv.Bp + r0 + r] = xv;
+      }
+    }
+    xs[idx] = x;
+    xs2[idx] = x2;
+    xa[idx] = xv;
+  }
   if (tid < 4) {
     const bool ok = tid < valid;
     const int sl = ok ? g.slots[r0 + tid] : 0;
