@@ -5,10 +5,11 @@
 // a tiled GEMM spends its time in prologue, epilogue and launch, and a VALU
 // kernel is LDS-bandwidth-bound (every fmaf operand pair comes from LDS).
 //
-// Here a workgroup (4 waves) owns a 64-row x 128-column output block.  The
-// K x 128 weight panel and the 64 x K input tile are split once into their
-// exact three bf16 planes (x = h + m + l) in LDS; each wave owns 32 rows x 64
-// columns (two 32x32 tiles) and takes the six plane products of the twin GEMM
+// Here a workgroup (4 waves) owns a 64-row x TK_COLS-column output block
+// (TK_COLS = 128, or 64 for a 48-KB block, three per CU).  The
+// K x TK_COLS weight panel and the 64 x K input tile are split once into their
+// exact three bf16 planes (x = h + m + l) in LDS; each wave owns 32 rows x
+// TK_COLS / 2 columns (TK_TPW 32x32 tiles) and takes the six plane products of the twin GEMM
 // (gemm_h.h) per 16-deep step on v_mfma_f32_32x32x16_bf16 with fp32
 // accumulation -- 2.7x the fp32-input MFMA rate at the same accuracy class as
 // the large GEMMs.  The fused epilogue has the gemm_common.h semantics (bias,
@@ -26,7 +27,16 @@
 namespace ddpg {
 
 constexpr int TK_MAXK = 64;
-constexpr int TK_ROWS = 64, TK_COLS = 128, TK_NT = 256;
+#ifndef TK_COLS_CFG
+#define TK_COLS_CFG 128
+#endif
+constexpr int TK_ROWS = 64, TK_COLS = TK_COLS_CFG, TK_NT = 256;
+static_assert(TK_COLS == 64 || TK_COLS == 128, "thin_k column block");
+constexpr int TK_TPW = TK_COLS / 64;       // 32x32 tiles per wave (4 waves: 2 x 2)
+constexpr int TK_KQS = TK_NT / TK_COLS;    // k-quad stride of the W panel loads
+constexpr int TK_WJ = 16 / TK_KQS;         // W panel float4 loads per thread
+constexpr int TK_OCT = TK_COLS / 8;        // column octets of the epilogue
+constexpr int TK_RG = TK_NT / TK_OCT;      // epilogue row groups
 constexpr int TK_KALIGN = 8;
 
 struct TkPart {
@@ -66,6 +76,7 @@ constexpr int TK_WIMG = TK_COLS * 128;  // bytes per W plane
 constexpr int TK_OUT_BYTES = TK_ROWS * TK_VLD * 4;
 constexpr int TK_WREG = 3 * TK_WIMG > TK_OUT_BYTES ? 3 * TK_WIMG : TK_OUT_BYTES;
 constexpr int TK_LDS = TK_WREG + 3 * TK_XIMG;
+static_assert(TK_RG * TK_COLS * 4 <= 3 * TK_XIMG, "column-sum scratch aliases the X image");
 DDPG_DEV int tk_swz(int r) { return (r >> 1) & 7; }
 DDPG_DEV int tk_off(int r, int k) { return r * 128 + 16 * ((k >> 3) ^ tk_swz(r)) + 2 * (k & 7); }
 
@@ -73,14 +84,15 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   // W image (3 planes), after the MFMAs the raw output tile [64 rows][TK_VLD];
   // then the X image (3 planes)
   __shared__ __attribute__((aligned(16))) char lds[TK_LDS];
-  __shared__ float red[16 * TK_COLS];
   float* const Ws = reinterpret_cast<float*>(lds);
   char* const wimg = lds;
   char* const ximg = lds + TK_WREG;
+  // column-sum scratch: the X image, dead after the MFMA phase
+  float* const red = reinterpret_cast<float*>(ximg);
   const TkPart P = blockIdx.z ? args.p[1] : args.p[0];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, h = lane >> 5;
-  const int wr = wave & 1, wc = wave >> 1;  // 32-row half, 64-column half
+  const int wr = wave & 1, wc = wave >> 1;  // 32-row half, column half
   const int m0 = blockIdx.y * TK_ROWS, n0 = blockIdx.x * TK_COLS;
   if (n0 >= P.N) return;
   TK_STAMP(0);
@@ -89,13 +101,13 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   const int KP = 16 * KS;
   // ---- global loads: thread (column c, k quads kq + 2 j) of the W panel, and
   // 4 float4 quads of the X tile (64 rows x 16 quads)
-  const int wcol = tid & 127, kq = tid >> 7, wn = n0 + wcol;
-  f32x4 wv[8], xg[4];
+  const int wcol = tid % TK_COLS, kq = tid / TK_COLS, wn = n0 + wcol;
+  f32x4 wv[TK_WJ], xg[4];
   {
     const bool wvec = P.w_nk && ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 4 * (kq + 2 * j);
+    for (int j = 0; j < TK_WJ; ++j) {
+      const int k = 4 * (kq + TK_KQS * j);
       wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < K && wn < P.N) {
         if (P.w_nk) {  // W[n][k]: 4 consecutive k (rows of an unaligned stride as scalars)
@@ -125,8 +137,8 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     *reinterpret_cast<bf16x4*>(img + 2 * plane_bytes + off) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
   };
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 4 * (kq + 2 * j);
+  for (int j = 0; j < TK_WJ; ++j) {
+    const int k = 4 * (kq + TK_KQS * j);
     if (k < KP) put4(wimg, TK_WIMG, wcol, k, wv[j]);
   }
 #pragma unroll
@@ -139,26 +151,26 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   // ---- MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulation): per 16-deep step
   // the six plane products hh, hm, mh, hl, lh, mm of gemm_h.h, the five small
   // ones in their own accumulator.  Wave (wr, wc): rows 32 wr + li, columns
-  // 64 wc + 32 t + li (t = 0, 1).
-  f32x16 acc[2], acs[2];
+  // (TK_COLS / 2) wc + 32 t + li (t < TK_TPW).
+  f32x16 acc[TK_TPW], acs[TK_TPW];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < TK_TPW; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = acs[t][r] = 0.f;
   const int ra = 32 * wr + li;
   for (int ks = 0; ks < KS; ++ks) {
     const int kk = 16 * ks + 8 * h;
-    bf16x8 a[3], b[2][3];
+    bf16x8 a[3], b[TK_TPW][3];
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       a[p] = *reinterpret_cast<const bf16x8*>(ximg + p * TK_XIMG + tk_off(ra, kk));
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < TK_TPW; ++t)
         b[t][p] = *reinterpret_cast<const bf16x8*>(wimg + p * TK_WIMG +
-                                                   tk_off(64 * wc + 32 * t + li, kk));
+                                                   tk_off((TK_COLS / 2) * wc + 32 * t + li, kk));
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < TK_TPW; ++t) {
       f32x16 q = acs[t];
       q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[t][0], q, 0, 0, 0);
       q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][1], q, 0, 0, 0);
@@ -170,7 +182,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     }
   }
 #pragma unroll
-  for (int t = 0; t < 2; ++t) acc[t] += acs[t];
+  for (int t = 0; t < TK_TPW; ++t) acc[t] += acs[t];
   TK_STAMP(2);
   // ---- epilogue.  The raw tile goes through LDS (lane li of tile t holds
   // column li, register r row (r & 3) + 8 (r >> 2) + 4 h) so that every
@@ -180,16 +192,16 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   {
     const int rb = 32 * wr + 4 * h;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < TK_TPW; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        Ws[(rb + (r & 3) + 8 * (r >> 2)) * TK_VLD + 64 * wc + 32 * t + li] = acc[t][r];
+        Ws[(rb + (r & 3) + 8 * (r >> 2)) * TK_VLD + (TK_COLS / 2) * wc + 32 * t + li] = acc[t][r];
   }
   __syncthreads();
   TK_STAMP(3);
   // thread -> column octet c8 = tid & 15, rows rg + 16 i (rg = tid >> 4):
   // 16-B fp32 and twin-plane stores
-  const int c8 = tid & 15, rg = tid >> 4, n = n0 + 8 * c8;
+  const int c8 = tid % TK_OCT, rg = tid / TK_OCT, n = n0 + 8 * c8;
   const bool q0 = n < P.N, q1 = n + 4 < P.N;  // N % 4 == 0: quads all in or all out
   const bool oct = q1 && ((P.ldo & 7) == 0) && ((P.hps & 7) == 0) &&
                    (((uintptr_t)P.outh & 15) == 0);
@@ -199,12 +211,12 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   float csum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-  constexpr int RPT = TK_ROWS / 16;  // rows per thread
+  constexpr int RPT = TK_ROWS / TK_RG;  // rows per thread
   f32x4 aq[RPT][2];
   if (P.aux) {  // all aux loads in flight before the first use
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const int m = m0 + rg + 16 * i;
+      const int m = m0 + rg + TK_RG * i;
       aq[i][0] = aq[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (m < M) {
         const float* ap = P.aux + (size_t)m * P.ldaux + n;
@@ -215,7 +227,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   }
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int rl = rg + 16 * i, m = m0 + rl;
+    const int rl = rg + TK_RG * i, m = m0 + rl;
     if (!q0 || m >= M) continue;
     f32x4 v[2];
     v[0] = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 8 * c8);
@@ -254,7 +266,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     if (tid < TK_COLS && n0 + tid < P.N) {
       float s = 0.f;
 #pragma unroll
-      for (int g = 0; g < 16; ++g) s += red[g * TK_COLS + tid];
+      for (int g = 0; g < TK_RG; ++g) s += red[g * TK_COLS + tid];
       P.colsum[(size_t)blockIdx.y * P.ld_colsum + n0 + tid] = s;
     }
   }
