@@ -1,15 +1,20 @@
 """Benchmark: DDPG actor+critic learner updates/s on MI355X (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5|c1]
+                  [--scaling weak|strong]
 
 One "step" = one whole learner update (ddpg.py:86-113) as ddpg_learner_step:
 host MT19937 draw of the batch from a replay ring filled to 1e6 synthetic
 transitions, device gather, target/critic/actor forward and
 backward, both Adam updates, both soft updates.  Inputs are resident in HBM
-before the timed region.  N>1: one process per GPU (torchrun), synchronous
-data parallelism, RCCL all-reduce of the critic then actor gradients, weak
-scaling (per-GPU batch fixed), value = batch-sized updates processed by all
-ranks / max-over-ranks time.
+before the timed region.  N>1: one process per GPU (launched by torchrun, or
+by this script itself when --gpus N > 1 and WORLD_SIZE is unset: it then
+starts N rank processes before touching the GPU and exits with the worst rank
+status), synchronous data parallelism, RCCL all-reduce of the critic then actor
+gradients.  --scaling weak (default): per-GPU batch fixed at the config's B,
+value = batch-B updates processed by all ranks / max-over-ranks time.
+--scaling strong: global batch fixed at B (B/N rows per GPU), value = global
+updates / s.
 
 Rank 0 prints ONE JSON line with the contract fields plus
   roofline      dominant kernel (HIP-event timed in-process) vs its MFMA peak (fp32:
@@ -18,7 +23,7 @@ Rank 0 prints ONE JSON line with the contract fields plus
                 (oracle/torch_cpu.py) on the host cores: 16 threads and 1 thread, + C2
   step_latency  p10 / median / p90 of per-step wall time (host sync after each step)
   small_batch   the InvertedPendulum B=64 latency-bound configuration (N=1 only)
-  c5_bf16       BASELINE configs[4] (S=376, A=17, 2048-wide, B=4096, bf16) (N=1, c3 only)
+  c5_bf16       BASELINE configs[4] (S=376, A=17, 2048-wide, B=4096, bf16) (c3 only; every N)
 """
 import argparse
 import json
@@ -42,8 +47,11 @@ CONFIGS = {
            "C2 InvertedPendulum-shaped S=4 A=1 128/200, batch 64"),
     "c5": (376, 17, 2048, 2048, 4096, 1.0,
            "C5 Humanoid-shaped S=376 A=17 2048/2048, batch 4096/GPU"),
+    # BASELINE configs[0]: MountainCar-shaped, 400/300 MLP, batch 64 (CPU leg)
+    "c1": (2, 1, 400, 300, 64, 1.0,
+           "C1 MountainCar-shaped S=2 A=1 400/300, batch 64"),
 }
-DEFAULT_DTYPE = {"c3": "fp32", "c2": "fp32", "c5": "bf16"}
+DEFAULT_DTYPE = {"c3": "fp32", "c2": "fp32", "c5": "bf16", "c1": "fp32"}
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # ~2.5 PF dense (MI355X_MICROARCH.md)
 # fp32 GEMMs on the bf16 pipe (gemm_s3): six bf16 MFMA products per fp32 MAC,
 # so the pipe bounds fp32-equivalent throughput at 2.5 PF / 6
@@ -55,11 +63,58 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="fp32"):
+def spawn_ranks(n):
+    """--gpus N > 1 without a launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, the same
+    arguments), before this process touches the GPU.  Rank 0 prints the JSON
+    line.  If a rank fails the others are stopped.  Returns the worst exit
+    status (0 when every rank succeeded)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [None] * n
+    first_bad = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            bad = [(i, rc) for i, rc in enumerate(rcs) if rc not in (None, 0)]
+            first_bad = bad[0][1]
+            log("[bench] rank(s) %s failed; stopping the others" % bad)
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.2)
+    # the status of the first rank that failed by itself; signal k -> 128 + k
+    rc = first_bad if first_bad is not None else next((r for r in rcs if r), 0)
+    return rc if rc >= 0 else 128 - rc
+
+
+def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="fp32",
+                  per_gpu_b=None):
     from distributed_ddpg_amd import networks as nets
     from distributed_ddpg_amd.learner import FusedLearner, fill_synthetic, init_comm
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
     S, A, H1, H2, B, scale, _ = CONFIGS[cfg_name]
+    B = per_gpu_b or B
     nets.reset_default_graph()
     actor = nets.ActorNetwork(S, A, scale, 1e-4, 1e-3, None, h1=H1, h2=H2)
     critic = nets.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), None, h1=H1,
@@ -127,10 +182,13 @@ def summarize_profile(rows, steps):
         k = by_kernel.setdefault(sym, {"ms": 0.0, "launches": 0, "flops": 0.0, "bytes": 0.0})
         for f in ("ms", "launches", "flops", "bytes"):
             k[f] += r[f]
-    gpu_ms = sum(r["ms"] for r in rows.values()) / steps
-    gemm_ms = sum(r["ms"] for k, r in by_kernel.items() if k.startswith("gemm")) / steps
-    gemm_flops = sum(r["flops"] for k, r in by_kernel.items() if k.startswith("gemm")) / steps
-    dom = max(by_kernel.items(), key=lambda kv: kv[1]["ms"])
+    # the collectives' events run on the comm stream concurrently with kernels:
+    # they are neither GPU-busy time nor a roofline candidate
+    comp = {k: v for k, v in by_kernel.items() if not k.startswith("rccl")}
+    gpu_ms = sum(r["ms"] for k, r in rows.items() if not k.startswith("rccl")) / steps
+    gemm_ms = sum(r["ms"] for k, r in comp.items() if k.startswith("gemm")) / steps
+    gemm_flops = sum(r["flops"] for k, r in comp.items() if k.startswith("gemm")) / steps
+    dom = max(comp.items(), key=lambda kv: kv[1]["ms"])
     return by_kernel, dom, gpu_ms, gemm_ms, gemm_flops
 
 
@@ -183,60 +241,87 @@ def _cpu_model():
     return cpu, cores
 
 
-def _cpu_leg(cfg_name, threads, budget_s, max_steps=200):
-    """Time the torch-CPU restatement of the reference's 8-sess.run learner
-    step (oracle/torch_cpu.py) at `threads` intra-op threads, bounded by
-    budget_s seconds or max_steps steps (whichever first, >= 1 step)."""
-    import random
+def _ref_replay(cfg_name, rows_n):
+    """The reference's deque replay (oracle/torch_cpu.py DequeReplay,
+    replay_buffer.py:12-47) filled with rows_n synthetic transitions."""
+    from oracle.torch_cpu import DequeReplay
+    S, A, _, _, _, scale, _ = CONFIGS[cfg_name]
+    rng = np.random.default_rng(0)
+    rb = DequeReplay(rows_n, seed=1234)
+    chunk = 100_000
+    for lo in range(0, rows_n, chunk):
+        m = min(chunk, rows_n - lo)
+        rb.fill(rng.standard_normal((m, S)), (rng.uniform(-1, 1, (m, A)) * scale).astype(np.float32),
+                rng.standard_normal(m), rng.random(m) < 0.01, rng.standard_normal((m, S)))
+    return rb
 
+
+def _cpu_leg(cfg_name, threads, budget_s, rb, max_steps=200):
+    """Time the reference's learner step on the CPU: replay_buffer.sample_batch
+    over a full deque (DequeReplay) + the torch-CPU restatement of the eight
+    sess.run calls (oracle/torch_cpu.py) at `threads` intra-op threads, bounded
+    by budget_s seconds or max_steps steps (whichever first, >= 1 step)."""
     import torch
     from oracle.torch_cpu import TorchCPULearner
     S, A, H1, H2, B, scale, _ = CONFIGS[cfg_name]
     torch.set_num_threads(threads)
     L = TorchCPULearner(S, A, H1, H2, scale, seed=1)
-    rng = np.random.default_rng(0)
-    pool = 20000
-    rows = (rng.standard_normal((pool, S), dtype=np.float32),
-            (rng.uniform(-1, 1, (pool, A)) * scale).astype(np.float32),
-            rng.standard_normal(pool, dtype=np.float32), rng.random(pool) < 0.01,
-            rng.standard_normal((pool, S), dtype=np.float32))
-    smp = random.Random(1234)   # replay_buffer.py's random.sample
-    L.step(*(x[np.array(smp.sample(range(pool), B))] for x in rows))  # warm-up
-    n, t0 = 0, time.perf_counter()
+    L.step(*rb.sample_batch(B))  # warm-up
+    n, t_sample, t0 = 0, 0.0, time.perf_counter()
     while True:
-        idx = np.array(smp.sample(range(pool), B))
-        L.step(*(x[idx] for x in rows))
+        ts = time.perf_counter()
+        batch = rb.sample_batch(B)
+        t_sample += time.perf_counter() - ts
+        L.step(*batch)
         n += 1
         el = time.perf_counter() - t0
         if el >= budget_s or n >= max_steps:
             break
     return {"value": round(n / el, 3), "unit": "updates/s", "threads": threads, "steps": n,
-            "seconds": round(el, 2)}
+            "seconds": round(el, 2), "sample_batch_ms": round(1e3 * t_sample / n, 3)}
 
 
 def cpu_baseline(cfg_name, threads):
     """the reference's TF CPU path cannot run on the GPU box, so
-    the baseline is a torch-CPU eager, op-for-op restatement of its eight
-    sess.run calls per learner step, timed on this host at `threads` threads and
-    at 1 thread, at the bench config and at C2 (B=64)."""
+    the baseline is the reference's own host replay sampling (deque +
+    random.sample + np.array stacking over a full 1e6-row buffer) plus a
+    torch-CPU eager, op-for-op restatement of its eight sess.run calls per
+    learner step, timed on this host at `threads` threads (the box's CPU
+    share), at 1 thread and at os.cpu_count() threads; at the bench config, at
+    C2 (B=64) and at C1 (BASELINE configs[0]: MountainCar-shaped 400/300,
+    B=64)."""
     import torch
     cpu, cores = _cpu_model()
+    allc = os.cpu_count() or 1
     prev = torch.get_num_threads()
-    main = _cpu_leg(cfg_name, threads, 12.0)
-    one = _cpu_leg(cfg_name, 1, 10.0)
-    c2 = _cpu_leg("c2", threads, 4.0, 2000)
-    c2_one = _cpu_leg("c2", 1, 4.0, 2000)
+    t0 = time.perf_counter()
+    rb = _ref_replay(cfg_name, REPLAY_ROWS)
+    fill_s = time.perf_counter() - t0
+    main = _cpu_leg(cfg_name, threads, 12.0, rb)
+    one = _cpu_leg(cfg_name, 1, 8.0, rb)
+    every = _cpu_leg(cfg_name, allc, 6.0, rb) if allc != threads else main
+    del rb
+    out = {}
+    for name in ("c2", "c1"):
+        rbs = _ref_replay(name, REPLAY_ROWS)
+        out[name + "_b64"] = _cpu_leg(name, threads, 3.0, rbs, 2000)
+        out[name + "_b64_one_thread"] = _cpu_leg(name, 1, 3.0, rbs, 2000)
+        del rbs
     torch.set_num_threads(prev)
-    return {"value": main["value"], "unit": "updates/s", "cores": threads, "kind": "port",
-            "sample": "%d learner steps of %s in %.1fs: torch-CPU fp32 eager restatement of the "
-                      "reference's 8 sess.run calls per step (oracle/torch_cpu.py; TF 1.3 is not "
-                      "installable on the box), %d threads on %s (%d physical cores on the host; "
-                      "the GPU box's CPU share is 16 threads)"
-                      % (main["steps"], cfg_name.upper(), main["seconds"], threads, cpu, cores),
-            "one_thread": one, "c2_b64": c2, "c2_b64_one_thread": c2_one,
-            "cpu_model": cpu, "host_cores": cores,
-            "historical_reference": "about 52 updates/s end to end incl. env + gRPC "
-                                    "(BASELINE.md, 2017 TF CPU; context only)"}
+    res = {"value": main["value"], "unit": "updates/s", "cores": threads, "kind": "port",
+           "sample": "%d learner steps of %s in %.1fs, each = the reference's sample_batch over "
+                     "a full %d-row deque (%.1f ms of it) + a torch-CPU fp32 eager restatement of "
+                     "its 8 sess.run calls (oracle/torch_cpu.py; TF 1.3 is not installable on the "
+                     "box), %d threads on %s (%d physical cores on the host, os.cpu_count() = %d; "
+                     "the GPU box's CPU share is 16 threads)"
+                     % (main["steps"], cfg_name.upper(), main["seconds"], REPLAY_ROWS,
+                        main["sample_batch_ms"], threads, cpu, cores, allc),
+           "one_thread": one, "all_cpus": every, "deque_fill_s": round(fill_s, 1),
+           "cpu_model": cpu, "host_cores": cores, "os_cpu_count": allc,
+           "historical_reference": "about 52 updates/s end to end incl. env + gRPC "
+                                   "(BASELINE.md, 2017 TF CPU; context only)"}
+    res.update(out)
+    return res
 
 
 def step_latency_percentiles(fl, sess, n):
@@ -265,14 +350,23 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=20)
     ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
                     help="GEMM operand precision (default: fp32, bf16 for c5)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: per-GPU batch fixed at the config's B; strong: global batch "
+                         "fixed at B (B/N rows per GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, before this process touches the GPU
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("[bench] note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     import torch
+    if local >= torch.cuda.device_count():
+        raise SystemExit("[bench] rank %d: LOCAL_RANK %d but only %d GPU(s) visible"
+                         % (rank, local, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
@@ -281,19 +375,26 @@ def main():
 
     cfg = args.config
     dtype = args.dtype or DEFAULT_DTYPE[cfg]
-    S, A, H1, H2, B, scale, label = CONFIGS[cfg]
+    S, A, H1, H2, B0, scale, label = CONFIGS[cfg]
+    strong = args.scaling == "strong"
+    if strong and B0 % world:
+        raise SystemExit("[bench] strong scaling: batch %d not divisible by %d GPUs" % (B0, world))
+    B = B0 // world if strong else B0   # rows per GPU
+    if strong:
+        label = label.replace("batch %d/GPU" % B0, "global batch %d (%d/GPU)" % (B0, B))
     label = "%s, %s GEMM operands (fp32 master weights/accumulation)" % (label, dtype)
-    sess, rb, fl, _ = build_learner(cfg, local, rank, world, args.replay, dtype=dtype)
+    sess, rb, fl, _ = build_learner(cfg, local, rank, world, args.replay, dtype=dtype, per_gpu_b=B)
     el = timed(fl, sess, args.steps, args.warmup, world)
     ms = 1000.0 * el / args.steps
-    value = world * args.steps / el   # batch-B updates processed by all ranks per second
+    # weak: batch-B updates processed by all ranks per second; strong: global updates per second
+    value = (1 if strong else world) * args.steps / el
 
     lat = step_latency_percentiles(fl, sess, min(100, max(10, args.steps)))
     rows, _ = kernel_profile(fl, sess, args.profile_steps)
     by_kernel, (dom_name, dom), gpu_ms, gemm_ms, gemm_flops = summarize_profile(
         rows, args.profile_steps)
     from distributed_ddpg_amd.flops import flops_per_step
-    step_flops = flops_per_step(S, A, H1, H2, B)
+    step_flops = flops_per_step(S, A, H1, H2, B)   # per GPU
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_flops = dom["flops"] / dom["launches"]
     achieved = dom_flops / (dom_avg_ms * 1e-3) / 1e12
@@ -304,7 +405,8 @@ def main():
     else:
         peak = PEAK_FP32_MFMA_TFLOPS
     step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
-    traffic, traffic_src = pmc_traffic(cfg, dom_name, dom["launches"] / args.profile_steps)
+    traffic, traffic_src = (pmc_traffic(cfg, dom_name, dom["launches"] / args.profile_steps)
+                            if world == 1 else (None, "PMC passes are single-GPU"))
     roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -314,17 +416,19 @@ def main():
                 "avg_launch_us": round(dom_avg_ms * 1e3, 2),
                 "flop_per_launch": dom_flops, "launches_per_step":
                     dom["launches"] / args.profile_steps}
+    metric = ("actor+critic updates/sec (global batch %d, %d-wide MLPs)" % (B0, H1) if strong else
+              "actor+critic updates/sec (batch %d per GPU, %d-wide MLPs)" % (B, H1))
     out = {
-        "metric": "actor+critic updates/sec (batch %d per GPU, %d-wide MLPs)" % (B, H1),
+        "metric": metric,
         "value": round(value, 3), "unit": "updates/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+        "scaling": args.scaling, "vs_baseline": None, "dtype": dtype,
         "data": "synthetic (replay ring of %d N(0,1)/U(-1,1)/Bernoulli(0.01) transitions; "
                 "random-init weights)" % args.replay,
         "config": {"workload": label, "state_dim": S, "action_dim": A, "hidden": [H1, H2],
                    "global_batch": B * world, "per_gpu_batch": B,
                    "parallelism": "dp%d" % world},
-        "samples_per_s": round(value * B, 1),
+        "samples_per_s": round(world * args.steps / el * B, 1),
         "mfma_util_step": round(step_flops / (ms * 1e-3) / 1e12 / step_peak, 4),
         "step_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
         "gemm_tflops": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else None,
@@ -340,6 +444,13 @@ def main():
                                  "per_step": v["launches"] / args.profile_steps}
                              for k, v in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])},
     }
+    if world > 1:
+        # the data-parallel exchange (rank 0's comm-stream events: these
+        # include waiting for the slowest rank); step_flops above are per GPU
+        out["exchange"] = {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
+                               "per_step": v["launches"] / args.profile_steps,
+                               "MB_per_step": round(v["bytes"] / args.profile_steps / 1e6, 3)}
+                           for k, v in by_kernel.items() if k.startswith("rccl")}
     hbm = {}
     for key in ("adam+soft_update", "adam", "soft_update", "gather"):
         if key in by_kernel and by_kernel[key]["ms"] > 0:
@@ -360,15 +471,17 @@ def main():
             "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1),
             "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
         s2.close()
-    if world == 1 and rank == 0 and not args.no_small and cfg == "c3":
-        # BASELINE configs[4] (C5, bf16) as a secondary line: same step, same
-        # accounting, its own dominant kernel
+    if not args.no_small and cfg == "c3":
+        # BASELINE configs[4] (C5, bf16) as a secondary line on every rank: same
+        # step, same accounting and scaling mode, its own dominant kernel
         sess.close()
-        s5, rb5, fl5, _ = build_learner("c5", local, 0, 1, args.replay, dtype="bf16")
-        el5 = timed(fl5, s5, 30, 5, 1)
+        S5, A5, H15, H25, B50, _, label5 = CONFIGS["c5"]
+        B5 = B50 // world if strong else B50
+        s5, rb5, fl5, _ = build_learner("c5", local, rank, world, args.replay, dtype="bf16",
+                                        per_gpu_b=B5)
+        el5 = timed(fl5, s5, 30, 5, world)
         rows5, _ = kernel_profile(fl5, s5, 10)
         bk5, (dn5, d5), gpu5, _, _ = summarize_profile(rows5, 10)
-        S5, A5, H15, H25, B5, _, label5 = CONFIGS["c5"]
         f5 = flops_per_step(S5, A5, H15, H25, B5)
         ms5 = 1000.0 * el5 / 30
         ach5 = (d5["flops"] / d5["launches"]) / (d5["ms"] / d5["launches"] * 1e-3) / 1e12
@@ -376,7 +489,9 @@ def main():
             else PEAK_FP32_MFMA_TFLOPS
         out["c5_bf16"] = {
             "workload": label5 + ", bf16 GEMM operands (fp32 master weights/accumulation)",
-            "value": round(30 / el5, 3), "unit": "updates/s", "ms_per_step": round(ms5, 4),
+            "value": round((1 if strong else world) * 30 / el5, 3), "unit": "updates/s",
+            "n_gpus": world, "per_gpu_batch": B5, "scaling": args.scaling,
+            "ms_per_step": round(ms5, 4),
             "dtype": "bf16", "gpu_busy_ms_per_step": round(gpu5, 4),
             "step_tflops": round(f5 / (ms5 * 1e-3) / 1e12, 2),
             "mfma_util_step": round(f5 / (ms5 * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS, 4),

@@ -226,9 +226,24 @@ struct ddpg_ctx {
   int sb_xstride = 1;         // XCD packing of the phase kernels (env DDPG_SB_XCD=1: on)
   unsigned long long* sb_stamps = nullptr;  // diagnostic (env DDPG_SB_STAMPS=1)
 
-  // comm
+  // kernel-path switches, read from the environment at ddpg_create (each is
+  // exercised by tests/test_gpu_switches.py)
+  struct {
+    bool gemm_h = true;    // DDPG_GEMM_H=0: no bf16-twin GEMM (gemm_s3 NP=3 instead)
+    bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
+    bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
+    int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
+    int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
+    bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
+  } sw;
+
+  // comm: every collective of the ctx is issued on cs (one stream, so the
+  // communicator sees them in the same order on every rank); cs forks from the
+  // producing stream and joins the consumer through the cev events
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
+  hipStream_t cs = nullptr;
+  hipEvent_t cev[8] = {};
 
   // profiling
   bool prof = false;
@@ -271,6 +286,7 @@ static void prof_collect(ddpg_ctx* c) {
   if (c->prof_recs.empty()) return;
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto st : c->aux) HIP_TRY(hipStreamSynchronize(st));
+  if (c->cs) HIP_TRY(hipStreamSynchronize(c->cs));
   for (auto& r : c->prof_recs) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, r.e0, r.e1));
@@ -296,7 +312,6 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Block-count target for tile selection (env DDPG_GEMM_MIN_BLOCKS overrides).
 static int g_min_blocks = 1024;
-static int g_xcd_remap = 1;  // env DDPG_XCD=0 disables
 
 struct GemmPlan {
   int bm = 128, bn = 128, splits = 1, kps = 0;
@@ -419,9 +434,6 @@ static void twins_refresh(ddpg_ctx* c) {
   c->wtw_ok = true;
 }
 
-// env DDPG_GEMM_H=0 keeps every GEMM off the bf16-twin kernel
-static int g_gemm_h = -1;
-static int g_gemm_mf = -1;
 
 template <int AL, int BL, int VA, int VB>
 static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const GemmArgs& g) {
@@ -440,13 +452,9 @@ static void gemm_dispatch(const GemmPlan& p, dim3 grid, hipStream_t st, const Ge
 // (H row panels of BM rows + W column panels of BN columns), when 8 such
 // rectangles tile the grid and it reads fewer bytes than the row-major runs.  env DDPG_XCD_RECT=0
 // keeps the runs.
-static int g_xcd_rect = -1;
-static int xcd_rect(int on, int nx, int ny, int BM, int BN) {
-  if (g_xcd_rect < 0) {
-    const char* v = getenv("DDPG_XCD_RECT");
-    g_xcd_rect = !(v && atoi(v) == 0);
-  }
-  if (!on || !g_xcd_rect || (nx * ny) % 8) return on;
+static int xcd_rect(const ddpg_ctx* c, int nx, int ny, int BM, int BN) {
+  const int on = c->sw.xcd;
+  if (!on || !c->sw.xcd_rect || (nx * ny) % 8) return on;
   const int T = nx * ny / 8;
   int best = -1, best_cost = 0;
   for (int W = 1; W <= nx; ++W) {
@@ -476,11 +484,7 @@ static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec);
 template <int AL, int BL>
 static bool gemm_h_ok(const ddpg_ctx* c, const float* A, int lda, const float* B, int ldb, int M,
                       int N, int K, int splits, int* Kh) {
-  if (g_gemm_h < 0) {
-    const char* v = getenv("DDPG_GEMM_H");
-    g_gemm_h = !(v && atoi(v) == 0);
-  }
-  if (!(g_gemm_h && c->hnp && M >= 128 && N >= 128 && N % 8 == 0 && lda % 8 == 0 &&
+  if (!(c->sw.gemm_h && c->hnp && M >= 128 && N >= 128 && N % 8 == 0 && lda % 8 == 0 &&
         ldb % 8 == 0 && (AL == L_RK || M % 8 == 0) && (BL == L_RK || N % 8 == 0)))
     return false;
   const int BKh = c->hnp == 1 ? 64 : 32;
@@ -560,15 +564,11 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       a.lda = lda;
       a.ldb = ldb;
       a.kps = h.kps;
-      a.xcd = xcd_rect(g_xcd_remap, h.nt(N), h.mt(M), BMh, HG_BN);
+      a.xcd = xcd_rect(c, h.nt(N), h.mt(M), BMh, HG_BN);
       a.e = ee;
       static const char* lay[2] = {"RK", "KR"};
       // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
-      if (g_gemm_mf < 0) {
-        const char* v = getenv("DDPG_GEMM_MF");
-        g_gemm_mf = (v && atoi(v) == 32) ? 32 : 16;
-      }
-      const bool h16 = c->hnp == 1 && g_gemm_mf == 16;
+      const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
       char key[112];
       snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s", h16 ? "gemm_h16_kernel" : "gemm_h_kernel",
                lay[AL], lay[BL], c->hnp, name);
@@ -600,7 +600,7 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   g.lda = lda;
   g.ldb = ldb;
   g.kps = p.kps;
-  g.xcd = g_xcd_remap;
+  g.xcd = c->sw.xcd;
   g.e = ee;
   dim3 grid(p.nt(N), p.mt(M), p.splits);
   // profile key "<kernel symbol>|<phase>": the symbol part matches rocprofv3's kernel names
@@ -641,19 +641,13 @@ static bool use_bf16(const ddpg_ctx* c, int M, int N, bool vec) {
 // fp32 contexts: the large GEMMs run fp32-accurate on the bf16 pipe
 // (gemm_s3.h, three-plane split); env DDPG_GEMM=f32 keeps every GEMM on the
 // fp32-input MFMA kernel.
-static int g_gemm_s3 = -1;
 static bool use_s3(const ddpg_ctx* c, int M, int N, bool vec) {
-  if (g_gemm_s3 < 0) {
-    const char* v = getenv("DDPG_GEMM");
-    g_gemm_s3 = !(v && strcmp(v, "f32") == 0);
-  }
-  return g_gemm_s3 && c->cfg.dtype == DDPG_FP32 && vec && M >= 128 && N >= 128;
+  return c->sw.gemm_s3 && c->cfg.dtype == DDPG_FP32 && vec && M >= 128 && N >= 128;
 }
 
 // Thin-K layers (thin_k.h) of fp32 contexts: K <= 64 and multiple of 8,
 // 4-aligned widths / leading dims, 16-byte aligned operands (anything else goes
 // through the GEMMs).  env DDPG_THINK=0 routes every such layer to the GEMMs.
-static int g_thin_k = -1;
 static bool tk_valid(const TkPart& q) {
   // W[n][k] (w_nk) may have any stride: the kernel loads it as scalars then
   return q.K >= TK_KALIGN && q.K % TK_KALIGN == 0 && q.K <= TK_MAXK && q.ldx % 4 == 0 &&
@@ -685,11 +679,7 @@ static TkPart tk_part(const float* X, int ldx, int K, const float* W, int ldw, i
 // (the row count of colsum partials), or 0 (nothing launched) when the layer
 // is not eligible and the caller must use the GEMM.
 static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M) {
-  if (g_thin_k < 0) {
-    const char* v = getenv("DDPG_THINK");
-    g_thin_k = !(v && atoi(v) == 0);
-  }
-  if (!g_thin_k) return 0;
+  if (!c->sw.thin_k) return 0;
   TkPart pp[2];
   for (int i = 0; i < nparts; ++i) {
     pp[i] = parts[i];
@@ -913,26 +903,59 @@ static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
   HIP_TRY(hipGetLastError());
 }
 
-static void allreduce(ddpg_ctx* c, float* buf, size_t n) {
-  if (c->world <= 1 || !c->comm) return;
-  ProfScope ps(c, "rccl_allreduce", 0, (double)n * 4.0);
-  ncclResult_t r = ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, c->comm, c->cur);
+static void nccl_try(ncclResult_t r) {
   if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
+}
+
+// `to` waits for the work queued so far on `from` (comm-stream events cev)
+static void cs_link(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
+  if (from == to) return;
+  HIP_TRY(hipEventRecord(c->cev[ev], from));
+  HIP_TRY(hipStreamWaitEvent(to, c->cev[ev], 0));
+}
+
+// In-place RCCL sums of up to 2 disjoint ranges of the flat grad buffer, on
+// the comm stream after the work queued so far on c->cur (one group: one
+// launch).  The caller joins cs back before the gradients are read.
+static void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0,
+                            float* b1 = nullptr, size_t n1 = 0) {
+  if (!c->comm) return;
+  cs_link(c, ev, c->cur, c->cs);
+  const hipStream_t prev = c->cur;
+  c->cur = c->cs;
+  {
+    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0);
+    nccl_try(ncclGroupStart());
+    if (n0) nccl_try(ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs));
+    if (n1) nccl_try(ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs));
+    nccl_try(ncclGroupEnd());
+  }
+  c->cur = prev;
 }
 
 // the logged stats of a data-parallel step are the
 // global-batch ones (ddpg.py:102-103) -- max over ranks of max(Q) and the sum
 // of the ranks' loss shares (each already scaled by 1/B_global).  One
 // all-gather of every rank's {q_max, loss}, then an ordered reduction that
-// every rank computes identically; it also feeds the running sums.
-static void stats_allreduce(ddpg_ctx* c) {
-  if (c->world <= 1 || !c->comm) return;
-  ProfScope ps(c, "rccl_stats", 0, 8.0 * c->world);
-  ncclResult_t r = ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cur);
-  if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cur, c->dstats_all, c->world,
-                     c->dstats, c->dacc);
-  HIP_TRY(hipGetLastError());
+// every rank computes identically; it also feeds the running sums.  On the
+// comm stream, after the critic all-reduce.
+static void stats_allreduce_on_cs(ddpg_ctx* c) {
+  if (!c->comm) return;
+  const hipStream_t prev = c->cur;
+  c->cur = c->cs;
+  {
+    ProfScope ps(c, "rccl_stats", 0, 8.0 * c->world);
+    nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cs, c->dstats_all, c->world,
+                       c->dstats, c->dacc);
+    HIP_TRY(hipGetLastError());
+  }
+  c->cur = prev;
+}
+
+// the consumer stream (c->cur) waits for every collective queued on cs
+static void join_cs(ddpg_ctx* c, int ev) {
+  if (c->comm) cs_link(c, ev, c->cs, c->cur);
 }
 
 // TF ApplyAdam over one network's flat region.  advance: also advance its
@@ -1035,6 +1058,17 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   GemmPlan pWh = gemm_launch<L_KR, L_KR>(c, "wgrad", c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1,
                                          c->CH2, B, e, 0, c->split_cap_Wh,
                                          c->grad + L.c[CWH].off);
+  float* G = c->grad;
+  const long long nWh = (long long)2 * c->CH1 * c->CH2;
+  if (c->comm) {
+    // data parallel: dWh (96 % of the critic's gradient bytes) is reduced and
+    // its all-reduce started now, under the dcat / dWs / dWa GEMMs below
+    ReduceTable t1;
+    t1.nseg = 0;
+    add_wgrad(t1, pWh, c->slab_Wh, G + L.c[CWH].off, nWh);
+    if (t1.nseg) reduce_launch(c, "grad_reduce", t1);
+    allreduce_on_cs(c, 0, "rccl_allreduce", G + L.c[CWH].off, (size_t)nWh);
+  }
   c->cur = main;
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
   e = epi_none();
@@ -1062,20 +1096,25 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
                                          c->grad + L.c[CWA].off);
   if (par) fork_to(c, 5, c->aux[0], main);  // join dWh
   // gather every critic gradient into the flat grad buffer
-  float* G = c->grad;
   ReduceTable tab;
   tab.nseg = 0;
   add_wgrad(tab, pWs, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1);
   add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, c->CH1);
   add_wgrad(tab, pWa, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1);
   add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, c->CH1);
-  add_wgrad(tab, pWh, c->slab_Wh, G + L.c[CWH].off, (long long)2 * c->CH1 * c->CH2);
+  if (!c->comm) add_wgrad(tab, pWh, c->slab_Wh, G + L.c[CWH].off, nWh);
   add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, c->CH2);
   add_seg(tab, part_dWo, G + L.c[CWO].off, c->CH2, nchunk, c->CH2);
   add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1);
   reduce_launch(c, "grad_reduce", tab);
-  allreduce(c, G + L.critic_begin, L.critic_end - L.critic_begin);
-  stats_allreduce(c);
+  if (c->comm) {
+    // the rest of the critic ([Ws bs Wa ba] and [bh Wo bo]) behind dWh on the
+    // comm stream, then the stats; Adam waits for all of it
+    allreduce_on_cs(c, 1, "rccl_allreduce", G + L.critic_begin, L.c[CWH].off - L.critic_begin,
+                    G + L.c[CBH].off, L.critic_end - L.c[CBH].off);
+    stats_allreduce_on_cs(c);
+    join_cs(c, 2);
+  }
   adam_launch(c, 1, !fused, fused);
 }
 
@@ -1149,6 +1188,16 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   e.out_split_stride = (long long)c->AH1 * c->AH2;
   GemmPlan pW2 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1,
                                          c->AH2, B, e, 0, c->split_cap_W2, G + L.a[AW2].off);
+  const long long nW2 = (long long)c->AH1 * c->AH2;
+  if (c->comm) {
+    // data parallel: dW2 (the bulk of the actor's gradient) reduced and its
+    // all-reduce started now, under the dz1 / dW1 GEMMs
+    ReduceTable t1;
+    t1.nseg = 0;
+    add_wgrad(t1, pW2, c->slab_W2, G + L.a[AW2].off, nW2);
+    if (t1.nseg) reduce_launch(c, "grad_reduce", t1);
+    allreduce_on_cs(c, 3, "rccl_allreduce", G + L.a[AW2].off, (size_t)nW2);
+  }
   c->cur = main;
   // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
   float* colpart1 = c->colpart + (size_t)mt2 * c->AH2;
@@ -1177,11 +1226,15 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   tab.nseg = 0;
   add_wgrad(tab, pW1, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1);
   add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, pz1.mt(B), c->AH1);
-  add_wgrad(tab, pW2, c->slab_W2, G + L.a[AW2].off, (long long)c->AH1 * c->AH2);
+  if (!c->comm) add_wgrad(tab, pW2, c->slab_W2, G + L.a[AW2].off, nW2);
   add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt2, c->AH2);
   add_wgrad(tab, pW3, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A);
   reduce_launch(c, "grad_reduce", tab);
-  allreduce(c, G + L.actor_begin, L.actor_end - L.actor_begin);
+  if (c->comm) {  // [W1 b1] and [b2 W3] behind dW2 on the comm stream
+    allreduce_on_cs(c, 4, "rccl_allreduce", G + L.actor_begin, L.a[AW2].off - L.actor_begin,
+                    G + L.a[AB2].off, L.actor_end - L.a[AB2].off);
+    join_cs(c, 5);
+  }
   adam_launch(c, 0, !fused, fused);
 }
 
@@ -1381,10 +1434,13 @@ static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B);
 
 // The fused learner step on this step's slots (c->d_slots): the small-batch
 // path (gather fused) or gather + the large-batch GEMM path.
+static bool takes_small(const ddpg_ctx* c, int B) {
+  return c->sb_ok && c->world == 1 && !c->comm && B <= c->sb_max_b;
+}
+
 static void learner_step_any(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
-  if (c->sb_ok && c->world == 1 && B <= c->sb_max_b) {
+  if (takes_small(c, B)) {
     learner_step_small(c, rb, B, inv_b);
-    c->wtw_ok = false;  // theta / target moved without their twins
   } else {
     gather_launch(c, rb, B);
     learner_step_dev(c, B, inv_b);
@@ -1459,6 +1515,9 @@ static void ctx_free(ddpg_ctx* c) {
     if (st) (void)hipStreamDestroy(st);
   for (auto ev : c->fj)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : c->cev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->cs) (void)hipStreamDestroy(c->cs);
   if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1559,7 +1618,18 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     const int mt = ceil_div(c->Bmax, std::min(64, TK_ROWS));  // row blocks of colsum partials
     const int nchunk = ceil_div(c->Bmax, std::min(kHeadRows, kHeadRows4));
     if (const char* mb = getenv("DDPG_GEMM_MIN_BLOCKS")) g_min_blocks = std::max(1, atoi(mb));
-    if (const char* xv = getenv("DDPG_XCD")) g_xcd_remap = atoi(xv) != 0;
+    {
+      auto env_is = [](const char* name, const char* val) {
+        const char* v = getenv(name);
+        return v && strcmp(v, val) == 0;
+      };
+      c->sw.gemm_h = !env_is("DDPG_GEMM_H", "0");
+      c->sw.gemm_s3 = !env_is("DDPG_GEMM", "f32");
+      c->sw.thin_k = !env_is("DDPG_THINK", "0");
+      c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
+      c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
+      c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
+    }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;
     c->split_cap_W3 = make_plan(c->AH2, c->A, c->Bmax, 0).splits;
@@ -1610,15 +1680,20 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       HIP_TRY(hipMalloc(&c->wtw, 2 * PT * c->hnp * sizeof(__bf16)));
       // the GEMM operands among the activations (gemm_h.h needs rows on
       // 16-B boundaries: ld % 8 == 0)
+      // w: the logical width.  Epilogue-written twins (w > 0) need it in whole
+      // 8-column groups, so the twin stores never reach the row padding; s / s2
+      // (w = 0) get their twins from the gather / upload, pads included.
       const struct {
         float* p;
-        int ld;
-      } tw[] = {{c->s, c->ldS},     {c->s2, c->ldS},     {c->h1, c->ldAH1},   {c->th1, c->ldAH1}, {c->cat, c->ldC},
-                {c->tcat, c->ldC},  {c->cat2, c->ldC},   {c->dhp, c->ldCH2}, {c->dhp2, c->ldCH2},
-                {c->dz2, c->ldAH2}, {c->dz1, c->ldAH1},  {c->dcat, c->ldC}};
-      for (const auto& t : tw)  // dh_pre's twin comes from the quad head kernel
-        if (t.ld % 8 == 0 && (t.p != c->dhp || c->CH2 % 4 == 0))
-          c->twinned.push_back({t.p, B * (size_t)t.ld});
+        int ld, w;
+      } tw[] = {{c->s, c->ldS, 0},           {c->s2, c->ldS, 0},
+                {c->h1, c->ldAH1, c->AH1},   {c->th1, c->ldAH1, c->AH1},
+                {c->cat, c->ldC, 2 * c->CH1}, {c->tcat, c->ldC, 2 * c->CH1},
+                {c->cat2, c->ldC, 2 * c->CH1}, {c->dhp, c->ldCH2, c->CH2},
+                {c->dhp2, c->ldCH2, c->CH2}, {c->dz2, c->ldAH2, c->AH2},
+                {c->dz1, c->ldAH1, c->AH1},  {c->dcat, c->ldC, 2 * c->CH1}};
+      for (const auto& t : tw)
+        if (t.ld % 8 == 0 && t.w % 8 == 0) c->twinned.push_back({t.p, B * (size_t)t.ld});
     }
     HIP_TRY(hipMalloc(&c->d_slots, B * sizeof(int)));
     HIP_TRY(hipHostMalloc(&c->h_slots, kSlotRing * B * sizeof(int)));
@@ -1828,6 +1903,8 @@ int ddpg_param_count(ddpg_ctx* c, int which, size_t* n) {
 
 int ddpg_set_params(ddpg_ctx* c, int which, const float* host, size_t n) {
   return guard(c, [&] {
+    if (which == DDPG_ACTOR_GRAD || which == DDPG_CRITIC_GRAD)
+      throw einval("param set %d (gradient) is get-only", which);
     const Tensor* ts;
     int nt;
     float* base;
@@ -2342,10 +2419,13 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   check_b(c, B);
   const int64_t* mine = idx + (size_t)c->rank * B;  // this rank's slice of the global draw
   const float inv_b = 1.0f / (float)Bg;
+  const bool small = takes_small(c, B);
   sb_refresh_shadows(c);
-  twins_refresh(c);
+  // the small path reads no twins: they are rebuilt lazily by the next
+  // large-batch call (every 1:1 method and large step calls twins_refresh)
+  if (!small) twins_refresh(c);
   // graphs: single-rank, not profiling (RCCL capture and per-kernel events stay eager)
-  if (c->use_graph && c->world == 1 && !c->prof) {
+  if (c->use_graph && c->world == 1 && !c->comm && !c->prof) {
     auto& g = c->gslot[c->gcur];
     c->gcur ^= 1;
     HIP_TRY(hipEventSynchronize(g.done));  // this slot's previous replay has finished
@@ -2384,9 +2464,13 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     learner_step_any(c, rb, B, inv_b);
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
-  // a large-path step (eager, or a graph replay that captured no host flag
-  // update) moved theta without refreshing the small path's W^T shadows
-  if (!(c->sb_ok && c->world == 1 && B <= c->sb_max_b)) c->sb_shadow_ok = false;
+  // Host-side state flags, updated here because a graph replay runs no host
+  // code: a large-path step moved theta without refreshing the small path's
+  // W^T shadows; a small-path step moved theta / target without their twins.
+  if (small)
+    c->wtw_ok = false;
+  else
+    c->sb_shadow_ok = false;
   if (stats) {
     float st[2];
     HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));
@@ -2447,13 +2531,19 @@ int ddpg_comm_init(ddpg_ctx* c, const char* id128, int world, int rank) {
   return guard(c, [&] {
     if (world != c->world || rank != c->rank)
       throw einval("comm (%d/%d) != cfg (%d/%d)", rank, world, c->rank, c->world);
-    if (world <= 1) return;
+    if (!id128) throw einval("null unique id");
+    if (c->comm) throw DdpgError(DDPG_ESTATE, "communicator already initialised");
+    // world == 1 makes a 1-rank communicator: the data-parallel exchange then
+    // runs (as an identity) through the same RCCL call sites as world > 1
     ncclUniqueId id;
     memcpy(&id, id128, 128);
     HIP_TRY(hipSetDevice(c->cfg.device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)world * sizeof(float)));
-    ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
-    if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
+    if (!c->cs) HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+    for (auto& ev : c->cev)
+      if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    nccl_try(ncclCommInitRank(&c->comm, world, id, rank));
   });
 }
 

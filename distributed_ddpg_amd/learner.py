@@ -20,12 +20,18 @@ def rccl_unique_id():
     return buf.raw
 
 
-def init_comm(sess, rank, world, pg=None):
+def init_comm(sess, rank, world, pg=None, single=False):
     """Create the RCCL communicator of this rank's context.  The 128-byte
     unique id is broadcast from rank 0 over torch.distributed (any backend;
     gloo in CPU tests).  This is the replacement of the reference's
-    tf.train.ClusterSpec/Server rendezvous (ddpg.py:168-174)."""
+    tf.train.ClusterSpec/Server rendezvous (ddpg.py:168-174).
+
+    world == 1 creates no communicator unless `single` is set: then a 1-rank
+    RCCL communicator runs the data-parallel exchange as an identity through
+    the same call sites as world > 1 (a one-GPU test of them)."""
     if world <= 1:
+        if single:
+            check(lib.ddpg_comm_init(sess.ctx, rccl_unique_id(), 1, 0), sess.ctx)
         return
     import torch.distributed as dist
     obj = [rccl_unique_id() if rank == 0 else None]

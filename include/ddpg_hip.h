@@ -205,6 +205,14 @@ int ddpg_read_stats(ddpg_ctx* ctx, double* q_max_sum, double* loss_sum, int64_t*
 /* ------------------------------------------------------------- multi-GPU */
 /* RCCL unique id (128 bytes) on rank 0; broadcast it out of band. */
 int ddpg_comm_unique_id(char* out128);
+/* Replaces tf.train.ClusterSpec/Server + replica_device_setter (ddpg.py:168-174).
+ * world/rank must equal the cfg's.  world == 1 creates a 1-rank communicator:
+ * the step then runs its exchanges through the same RCCL call sites (identity
+ * sums), eagerly and on the large-batch path -- a test of those call sites on
+ * one GPU; without a communicator a world == 1 ctx issues no collectives.
+ * The exchanges run on a library-owned comm stream: the dWh (critic) and dW2
+ * (actor) all-reduces start as soon as those gradients are reduced, under the
+ * remaining backward GEMMs; each network's Adam waits for its exchange. */
 int ddpg_comm_init(ddpg_ctx* ctx, const char* id128, int world, int rank);
 
 /* ------------------------------------------------------------- profiling */

@@ -6,6 +6,7 @@ The reference runs ddpg.py:86-113 as eight TF 1.3 CPU `sess.run` calls
 (TF and the reference cannot run on the GPU box).  This mirrors those calls op
 for op in torch eager fp32 on the CPU, without the gRPC hops:
 
+  0 replay_buffer.sample_batch(B)       replay_buffer.py:33-47 (DequeReplay below)
   1 actor.predict_target(s2)            networks.py:82-85
   2 critic.predict_target(s2, a2)       networks.py:183-187
     y = r + gamma * q'  (numpy, ddpg.py:92-97)
@@ -19,12 +20,42 @@ Gradients come from torch autograd over the same dataflow TF's gradients
 built (grad_ys = -a_gradient for the actor, ones for dQ/da); ApplyAdam is TF's
 epsilon-hat form.
 """
+import random
+from collections import deque
+
 import numpy as np
 import torch
 
 from .ddpg_oracle import init_params
 
 F = torch.nn.functional
+
+
+class DequeReplay:
+    """The reference's host replay buffer, restated for the CPU baseline's
+    timing (replay_buffer.py:12-47): a bounded deque of per-transition tuples
+    (s float64 [S], a float32 [A], r float, t bool, s2 float64 [S]), sampled
+    by the stdlib's random.sample over the deque itself (deque indexing is
+    O(n/64) per element) and stacked into five arrays with np.array.  This is
+    the host cost the reference pays in step 1 of every learner update
+    (ddpg.py:88), measured at 0.85 / 2.9 / 46.8 ms for B = 64 / 256 / 4096 on a
+    full 1e6 deque."""
+
+    def __init__(self, capacity, seed=1234):
+        self.buf = deque(maxlen=int(capacity))
+        self.rng = random.Random(seed)
+
+    def fill(self, s, a, r, t, s2):
+        """Append rows (row views of the given arrays stand in for the env's
+        per-step arrays; np.array stacks views exactly as it stacks copies)."""
+        self.buf.extend(zip(list(s), list(a), [float(x) for x in r], [bool(x) for x in t],
+                            list(s2)))
+
+    def sample_batch(self, batch_size):
+        rows = self.rng.sample(self.buf, batch_size)
+        return (np.array([x[0] for x in rows]), np.array([x[1] for x in rows]),
+                np.array([x[2] for x in rows]), np.array([x[3] for x in rows]),
+                np.array([x[4] for x in rows]))
 
 
 def _elu(x):

@@ -1,10 +1,11 @@
-"""GPU parity against the reference's own executed TF graph.
+"""GPU parity against the reference's own executed TF graphs.
 
-The fixture tests/golden/graph_ip1410.npz is a 3-step trajectory of the
-reference's InvertedPendulum graph (model-1410.meta) executed from its own
-checkpoint -- weights, targets, Adam slots at t ~ 1.4e5 steps and beta powers
-(see tests/test_graph_pin.py for how it pins the oracle).  Here the HIP path
-reproduces it twice:
+Three fixtures (tests/test_graph_pin.py describes them and how they pin the
+oracle): graph_ip1410.npz (InvertedPendulum graph from its checkpoint),
+graph_ip1410_fresh.npz (the same with the graph's own optimizer initializers:
+Adam bias correction, alpha = 0.316 lr on step 1) and graph_mc120.npz (the
+MountainCar graph, S=2, actor 48/64 vs critic 48/128, states through a fitted
+scaler).  For each, the HIP path reproduces the 3-step trajectory twice:
   * through the 1:1 C-ABI methods in the exact ddpg.py:86-113 call order
     (predict_target x2, critic.train, predict, action_gradients, actor.train,
     update_target_network x2), reading back each gradient the library applied;
@@ -16,7 +17,7 @@ Bars as everywhere: forward outputs 1e-5, gradients / parameters / Adam slots
 import numpy as np
 import pytest
 
-from test_graph_pin import load_fixture_learner, rel
+from test_graph_pin import FIXTURES, fixture, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -29,15 +30,16 @@ def O():
     return ddpg_oracle
 
 
-def _session(O):
+def _session(O, name):
     import torch
     assert torch.cuda.is_available()
     import distributed_ddpg_amd.networks as nets
     from distributed_ddpg_amd import _lib
-    _, p, z = load_fixture_learner(O)
+    z, (S, A, H1, H2, CH1, CH2, scale), p, scaler = fixture(name)
     nets.reset_default_graph()
-    actor = nets.ActorNetwork(4, 1, 3.0, 1e-4, 1e-3, None)
-    critic = nets.CriticNetwork(4, 1, 1e-3, 1e-3, actor.get_num_trainable_vars(), None)
+    actor = nets.ActorNetwork(S, A, scale, 1e-4, 1e-3, scaler, h1=H1, h2=H2)
+    critic = nets.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), scaler,
+                                h1=CH1, h2=CH2)
     sess = nets.Session(batch_max=64)
     actor.set_session(sess)
     critic.set_session(sess)
@@ -71,9 +73,10 @@ def _check_final(O, sess, z):
         assert b2p == pytest.approx(float(z["final/beta2_power" + sfx]), rel=1e-6)
 
 
-def test_one_to_one_methods_follow_reference_graph(O):
+@pytest.mark.parametrize("name", list(FIXTURES))
+def test_one_to_one_methods_follow_reference_graph(O, name):
     from distributed_ddpg_amd import _lib
-    sess, actor, critic, z = _session(O)
+    sess, actor, critic, z = _session(O, name)
     for step in range(3):
         p = "step%d/" % step
         s, a, r, t, s2 = (z[p + k] for k in ("s", "a", "r", "t", "s2"))
@@ -98,11 +101,12 @@ def test_one_to_one_methods_follow_reference_graph(O):
     sess.close()
 
 
-def test_fused_step_follows_reference_graph(O):
+@pytest.mark.parametrize("name", list(FIXTURES))
+def test_fused_step_follows_reference_graph(O, name):
     from distributed_ddpg_amd import _lib
     from distributed_ddpg_amd.learner import FusedLearner
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
-    sess, actor, critic, z = _session(O)
+    sess, actor, critic, z = _session(O, name)
     rb = ReplayBuffer(3 * 64, 1234)
     for step in range(3):
         p = "step%d/" % step

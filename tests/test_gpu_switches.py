@@ -1,0 +1,226 @@
+"""GPU tests of every environment-selected kernel path, of the RCCL call sites
+of the data-parallel step (through a 1-rank communicator), and of the bf16
+twins after small-batch steps.  All calls go through the C-ABI.
+
+Switches (read at ddpg_create, so each session below sees its own setting):
+  placement only -- results must be BITWISE equal to the default:
+    DDPG_XCD=0        no XCD-aware tile order
+    DDPG_XCD_RECT=0   row-major XCD runs instead of per-XCD tile rectangles
+    DDPG_PAR=1        independent branches forked onto two aux streams
+    DDPG_SB_XCD=1     small-batch workgroups packed on one XCD
+    DDPG_GEMM_MF=32   bf16 config on the 32x32x16 twin GEMM (same per-output
+                      summation order as the default 16x16x32 kernel)
+  different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
+    DDPG_GEMM=f32     every GEMM on the fp32-input MFMA kernel (no twins)
+    DDPG_GEMM_H=0     no twins; large GEMMs on gemm_s3 (operands split while staging)
+    DDPG_THINK=0      the K <= 64 layers on the tiled GEMMs instead of thin_k
+"""
+import random
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import (CONFIGS, GRAD_TOL, FWD_TOL, _fill, _params, _session,
+                             _session_dtype, assert_steps_close, f64, rel)
+
+pytestmark = pytest.mark.gpu
+
+SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
+            "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL")
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ddpg_oracle
+    return ddpg_oracle
+
+
+@pytest.fixture(scope="module")
+def dd():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import distributed_ddpg_amd.networks as nets
+    return nets
+
+
+def _clear(monkeypatch):
+    for k in SWITCHES:
+        monkeypatch.delenv(k, raising=False)
+
+
+def _run(dd, O, name, p, steps, dtype="fp32", seed=2, profile=False, comm=False):
+    """`steps` fused steps on a fresh session; returns the final state, the
+    per-step stats and (profile=True) the profiled kernel keys."""
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner, Profile, init_comm
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    if dtype == "fp32":
+        sess, actor, critic = _session(dd, O, name, p)
+    else:
+        sess, actor, critic = _session_dtype(dd, O, name, p, dtype)
+    if comm:
+        init_comm(sess, 0, 1, single=True)
+    rb = ReplayBuffer(5000, 1234)
+    rows = _fill(rb, S, A, 3000, scale, seed=seed)
+    fl = FusedLearner(sess, rb, B)
+    prof = Profile(sess)
+    if profile:
+        prof.enable(True)
+    st = [fl.step(stats=True) for _ in range(steps)]
+    keys = sorted(prof.read()) if profile else []
+    if profile:
+        prof.enable(False)
+    state = [sess.get_params(w) for w in (_lib.ACTOR, _lib.CRITIC, _lib.ACTOR_TARGET,
+                                          _lib.CRITIC_TARGET, _lib.ACTOR_ADAM_M, _lib.ACTOR_ADAM_V,
+                                          _lib.CRITIC_ADAM_M, _lib.CRITIC_ADAM_V, _lib.ACTOR_GRAD,
+                                          _lib.CRITIC_GRAD)]
+    powers = (sess.get_adam_powers(0), sess.get_adam_powers(1))
+    acc = fl.read_stats()
+    sess.close()
+    return {"state": state, "stats": st, "powers": powers, "acc": acc, "keys": keys,
+            "rows": rows}
+
+
+def _bitwise(a, b):
+    assert a["stats"] == b["stats"]
+    assert a["powers"] == b["powers"]
+    assert a["acc"] == b["acc"]
+    for x, y in zip(a["state"], b["state"]):
+        for u, v in zip(x, y):
+            assert np.array_equal(u, v)
+
+
+def _oracle(O, name, p, rows, steps):
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    L32 = O.Learner(S, A, H1, H2, scale, dtype=np.float32, params=p, init_blend=False)
+    rr = random.Random(1234)
+    for _ in range(steps):
+        idx = np.array(rr.sample(range(3000), B))
+        L.step(*(x[idx] for x in rows))
+        L32.step(*(x[idx] for x in rows))
+    return L, L32
+
+
+@pytest.mark.parametrize("switch,value,name", [
+    ("DDPG_XCD", "0", "wide"),
+    ("DDPG_XCD_RECT", "0", "wide"),
+    ("DDPG_PAR", "1", "wide"),
+    ("DDPG_SB_XCD", "1", "ip"),
+])
+def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
+    _clear(monkeypatch)
+    p, _ = _params(O, name)
+    ref = _run(dd, O, name, p, 3)
+    monkeypatch.setenv(switch, value)
+    got = _run(dd, O, name, p, 3)
+    _bitwise(got, ref)
+
+
+def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
+    """bf16 configuration: the 32x32x16 twin GEMM (DDPG_GEMM_MF=32) against the
+    default 16x16x32 kernel -- bitwise -- and against the oracle at the stated
+    bf16 bar."""
+    _clear(monkeypatch)
+    p, _ = _params(O, "wide")
+    ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
+    assert any(k.startswith("gemm_h16_kernel") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_GEMM_MF", "32")
+    got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
+    assert any(k.startswith("gemm_h_kernel") and "NP=1" in k for k in got["keys"]), got["keys"]
+    assert not any(k.startswith("gemm_h16_kernel") for k in got["keys"]), got["keys"]
+    _bitwise(got, ref)
+
+
+@pytest.mark.parametrize("switch,value,kernel,absent", [
+    ("DDPG_GEMM", "f32", "gemm_f32_kernel", "gemm_h"),
+    ("DDPG_GEMM_H", "0", "gemm_s3_kernel", "gemm_h"),
+    ("DDPG_THINK", "0", "gemm_h_kernel", "thin_k_kernel"),
+])
+def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent):
+    """A switch that selects different kernels: 3 fused steps at the 1024-wide
+    config still meet the oracle's fp32 bars, on the kernels it names."""
+    _clear(monkeypatch)
+    monkeypatch.setenv(switch, value)
+    name = "wide"
+    p, _ = _params(O, name)
+    got = _run(dd, O, name, p, 3, profile=True)
+    assert any(k.startswith(kernel) for k in got["keys"]), got["keys"]
+    assert not any(k.startswith(absent) for k in got["keys"]), got["keys"]
+    L, L32 = _oracle(O, name, p, got["rows"], 3)
+    nets = (("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS), ("actor_t", O.ACTOR_KEYS),
+            ("critic_t", O.CRITIC_KEYS))
+    for (net, keys), vals in zip(nets, got["state"][:4]):
+        for k, v in zip(keys, vals):
+            assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (switch, net, k))
+
+
+def test_single_rank_communicator_matches_no_communicator(dd, O, monkeypatch):
+    """The data-parallel exchange through RCCL (ncclAllReduce of the critic's
+    dWh then the rest, the stats ncclAllGather + stats_reduce_kernel, the
+    actor's dW2 then the rest, all on the comm stream) with a 1-rank
+    communicator is an identity: gradients, Adam slots, parameters, stats and
+    the running sums equal the communicator-less step BITWISE.  B = 1024 keeps
+    both runs on the large-batch path (a communicator always takes it)."""
+    _clear(monkeypatch)
+    name = "wide"
+    p, _ = _params(O, name)
+    S, A, H1, H2, scale, _, src = CONFIGS[name]
+    CONFIGS["wide_b1024"] = (S, A, H1, H2, scale, 1024, src)
+    try:
+        ref = _run(dd, O, "wide_b1024", p, 3, profile=True)
+        got = _run(dd, O, "wide_b1024", p, 3, profile=True, comm=True)
+    finally:
+        del CONFIGS["wide_b1024"]
+    assert not any(k.startswith("rccl") for k in ref["keys"]), ref["keys"]
+    assert "rccl_allreduce" in got["keys"] and "rccl_stats" in got["keys"], got["keys"]
+    _bitwise(got, ref)
+
+
+def test_twins_current_after_small_path_graph_steps(dd, O, monkeypatch):
+    """Small-batch fused steps (hipGraph-replayed, B = 64) move theta / theta'
+    without their bf16 twins; the next large-batch call must rebuild them.
+    Several replays, then predict / predict_target / critic.predict at
+    B = 256 (the twin GEMM path) against the oracle on the current params."""
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    _clear(monkeypatch)
+    name = "ip"
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    sess, actor, critic = _session(dd, O, name, p, batch_max=512)
+    rb = ReplayBuffer(4000, 3)
+    _fill(rb, S, A, 3000, scale, seed=6)
+    fl = FusedLearner(sess, rb, B)
+    rng = np.random.default_rng(17)
+    s = rng.standard_normal((256, S)).astype(np.float32)
+    a = (rng.uniform(-1, 1, (256, A)) * scale).astype(np.float32)
+    for rounds in range(3):
+        # raise the learning signal so the params move well past fp32 rounding
+        for _ in range(4):
+            fl.step()
+        cur = {"actor": dict(zip(O.ACTOR_KEYS, sess.get_params(_lib.ACTOR))),
+               "actor_t": dict(zip(O.ACTOR_KEYS, sess.get_params(_lib.ACTOR_TARGET))),
+               "critic": dict(zip(O.CRITIC_KEYS, sess.get_params(_lib.CRITIC)))}
+        mu = actor.predict(s)
+        assert rel(mu, O.actor_forward(f64(cur["actor"]), s.astype(np.float64), scale)[3]) < FWD_TOL
+        mut = actor.predict_target(s)
+        assert rel(mut, O.actor_forward(f64(cur["actor_t"]), s.astype(np.float64),
+                                        scale)[3]) < FWD_TOL
+        q = critic.predict(s, a)
+        assert rel(q, O.critic_forward(f64(cur["critic"]), s.astype(np.float64),
+                                       a.astype(np.float64))[3]) < FWD_TOL
+    sess.close()
+
+
+def test_gradient_sets_are_get_only(dd, O):
+    from distributed_ddpg_amd import _lib
+    p, _ = _params(O, "ip")
+    sess, actor, critic = _session(dd, O, "ip", p)
+    for which in (_lib.ACTOR_GRAD, _lib.CRITIC_GRAD):
+        g = sess.get_params(which)
+        with pytest.raises(RuntimeError, match="get-only"):
+            sess.set_params(which, g)
+    sess.close()
