@@ -396,8 +396,13 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h16_kernel(GemmHArgs g) {
   constexpr int TA = BM / 32;        // 16-row A fragments per wave
   constexpr int TB = 2;              // 16-column B fragments per wave
   constexpr int KS = BK / 32;
-  // NP = 3 holds 2 x 3 planes x 6 fragments of a 32-deep step: past 256 VGPRs
-  // (it spilled to scratch), so the fp32 configuration keeps gemm_h_kernel
+  // NP = 3 holds 2 x 3 planes x 6 fragments of a 32-deep step: past 256 VGPRs.
+  // It spilled, and the spills touched fragment registers whose inline-asm LDS
+  // reads were still in flight: the late LDS return overwrote a register the
+  // allocator had reused for a staging address -> the round-2 aperture
+  // violation (profiles/r3/np3_h16_fault_cause.txt).  tools/isa_check.py now
+  // rejects any build with scratch or such a hazard; the fp32 configuration
+  // keeps gemm_h_kernel.
   static_assert(NP == 1, "16x16x32 variant: one plane (bf16 configuration) only");
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM_BYTES / 4];
   char* const lds = reinterpret_cast<char*>(smem);

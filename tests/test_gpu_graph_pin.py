@@ -57,16 +57,53 @@ def _session(O, name):
     return sess, actor, critic, z
 
 
-def _check_final(O, sess, z):
+# fp32 resolution of a B = 64-term batch-sum gradient, relative to the tensor's
+# largest gradient: B * 2^-24
+SUM_RES = 64 * 2.0 ** -24
+
+
+def _determined(z, n, steps=3):
+    """Elements of parameter n whose Adam updates fp32 arithmetic determines:
+    |g| above the fp32 resolution of the batch sum (SUM_RES * max|g|) at every
+    step.  With fresh Adam state (v ~ g^2) the update of an element is
+    ~lr * g / |g|: for a near-cancelling batch sum below that resolution its
+    sign is rounding noise in ANY fp32 implementation -- the TF-semantics fp32
+    restatement (oracle in float32) itself lands up to 0.73 lr off the float64
+    fixture on exactly those elements (3.9e-4 max-rel on bh)."""
+    ok = None
+    for s in range(steps):
+        g = np.abs(z["step%d/grad/%s" % (s, n)].astype(np.float64))
+        m = g > SUM_RES * g.max()
+        ok = m if ok is None else ok & m
+    return ok
+
+
+def _check_final(O, sess, z, fresh=False, lr=None):
+    """Final state vs the fixture, max-rel 1e-4 per tensor.  fresh: online
+    parameters (and their targets) are checked at 1e-4 over the elements the
+    gradients determine (_determined: 93-100 % of each tensor); every other
+    element must stay within Adam's step bound of the fixture (2 lr per step)."""
     from distributed_ddpg_amd import _lib
-    for which, names in ((_lib.ACTOR, O.CKPT_ACTOR), (_lib.ACTOR_TARGET, O.CKPT_ACTOR_T),
-                         (_lib.CRITIC, O.CKPT_CRITIC), (_lib.CRITIC_TARGET, O.CKPT_CRITIC_T),
-                         (_lib.ACTOR_ADAM_M, [n + "/Adam" for n in O.CKPT_ACTOR]),
-                         (_lib.ACTOR_ADAM_V, [n + "/Adam_1" for n in O.CKPT_ACTOR]),
-                         (_lib.CRITIC_ADAM_M, [n + "/Adam" for n in O.CKPT_CRITIC]),
-                         (_lib.CRITIC_ADAM_V, [n + "/Adam_1" for n in O.CKPT_CRITIC])):
-        for n, v in zip(names, sess.get_params(which)):
-            assert rel(v, z["final/" + n]) < GRAD_TOL, n
+    for which, names, src in ((_lib.ACTOR, O.CKPT_ACTOR, O.CKPT_ACTOR),
+                              (_lib.ACTOR_TARGET, O.CKPT_ACTOR_T, O.CKPT_ACTOR),
+                              (_lib.CRITIC, O.CKPT_CRITIC, O.CKPT_CRITIC),
+                              (_lib.CRITIC_TARGET, O.CKPT_CRITIC_T, O.CKPT_CRITIC),
+                              (_lib.ACTOR_ADAM_M, [n + "/Adam" for n in O.CKPT_ACTOR], None),
+                              (_lib.ACTOR_ADAM_V, [n + "/Adam_1" for n in O.CKPT_ACTOR], None),
+                              (_lib.CRITIC_ADAM_M, [n + "/Adam" for n in O.CKPT_CRITIC], None),
+                              (_lib.CRITIC_ADAM_V, [n + "/Adam_1" for n in O.CKPT_CRITIC], None)):
+        for i, (n, v) in enumerate(zip(names, sess.get_params(which))):
+            ref = z["final/" + n].reshape(v.shape)
+            if not (fresh and src):
+                assert rel(v, ref) < GRAD_TOL, n
+                continue
+            det = _determined(z, src[i]).reshape(v.shape)
+            assert det.mean() > 0.9, (n, det.mean())
+            den = max(np.max(np.abs(ref)), 1e-30)
+            err = np.abs(v.astype(np.float64) - ref)
+            assert np.max(err[det]) / den < GRAD_TOL, n
+            step = 2 * 3 * (lr[0] if which in (_lib.ACTOR, _lib.ACTOR_TARGET) else lr[1])
+            assert np.all(err[~det] <= step), (n, np.max(err[~det], initial=0))
     for net, sfx in ((0, ""), (1, "_1")):
         b1p, b2p = sess.get_adam_powers(net)
         assert b1p == pytest.approx(float(z["final/beta1_power" + sfx]), rel=1e-6)
@@ -97,7 +134,7 @@ def test_one_to_one_methods_follow_reference_graph(O, name):
             assert rel(g, z[p + "grad/" + n]) < GRAD_TOL, (step, n)
         actor.update_target_network()                                           # ddpg.py:112
         critic.update_target_network()                                          # ddpg.py:113
-    _check_final(O, sess, z)
+    _check_final(O, sess, z, fresh=name.endswith("fresh"), lr=(1e-4, 1e-3))
     sess.close()
 
 
@@ -121,5 +158,5 @@ def test_fused_step_follows_reference_graph(O, name):
         for which, names in ((_lib.CRITIC_GRAD, O.CKPT_CRITIC), (_lib.ACTOR_GRAD, O.CKPT_ACTOR)):
             for n, g in zip(names, sess.get_params(which)):
                 assert rel(g, z[p + "grad/" + n]) < GRAD_TOL, (step, n)
-    _check_final(O, sess, z)
+    _check_final(O, sess, z, fresh=name.endswith("fresh"), lr=(1e-4, 1e-3))
     sess.close()
