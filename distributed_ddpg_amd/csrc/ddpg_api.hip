@@ -581,7 +581,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       else if (c->hnp == 1)
         hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else
-        hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 3, 128, 32>), grid, dim3(HG_NT), 0, c->cur, a);
+        // SCH 1: fragment reads spread over the MFMA gaps (+2-4 % over the
+        // burst schedule, bitwise equal; profiles/r3/gemmh_sched_c3.txt)
+        hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 3, 128, 32, 1>), grid, dim3(HG_NT), 0, c->cur, a);
       HIP_TRY(hipGetLastError());
       return h;
     }
@@ -606,10 +608,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
   // profile key "<kernel symbol>|<phase>": the symbol part matches rocprofv3's kernel names
   static const char* lay[2] = {"RK", "KR"};
   char key[112];
-  if (bf)
-    snprintf(key, sizeof key, "gemm_bf16_kernel<%s,%s>|%s", lay[AL], lay[BL], name);
-  else if (s3)
-    snprintf(key, sizeof key, "gemm_s3_kernel<%s,%s>|%s", lay[AL], lay[BL], name);
+  if (bf || s3)  // one bf16 plane (bf16 configuration) or the exact three-plane split
+    snprintf(key, sizeof key, "gemm_s3_kernel<%s,%s,NP=%d>|%s", lay[AL], lay[BL], bf ? 1 : 3,
+             name);
   else
     snprintf(key, sizeof key, "gemm_f32_kernel<%s,%s,%d,%d,%d,%d>|%s", lay[AL], lay[BL],
              va ? 4 : 1, vb ? 4 : 1, p.bm, p.bn, name);

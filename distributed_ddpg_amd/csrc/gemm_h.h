@@ -212,7 +212,12 @@ DDPG_DEV void hg_wait16(bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
 // are in different phases) is 15-25 % SLOWER on every C3/C5 shape than two
 // tiles in flight without a stagger: the glds latency under full load, not
 // the phase pairing, is what the second tile in flight covers.
-template <int AL, int BL, int NP, int BM, int BK>
+//
+// SCH = 1: the fragment reads of step ks+1 are spread between the MFMAs of
+// step ks (two read groups per MFMA gap, in program order pinned by
+// sched_barriers) instead of issued as one burst ahead of them, and the
+// tile-(t+2) glds sit in the MFMA gaps after the reads.
+template <int AL, int BL, int NP, int BM, int BK, int SCH = 0>
 __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   using C = HgCfg<BM, BK, NP>;
   constexpr int TM = BM / 64;
@@ -300,6 +305,28 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
     acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
   };
 
+  // read group j (0 .. NP * (TM + 1) - 1) of step ks: plane j / (TM + 1),
+  // fragment j % (TM + 1) (0: the B fragment, 1 ..: A fragment i - 1)
+  auto read_one = [&](const char* base, int ks, int j, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+    const int p = j / (TM + 1), f = j % (TM + 1);
+    if (f == 0)
+      bv[p] = hg_frag<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * 32, ks, lane);
+    else
+      av[p][f - 1] = hg_frag<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 32 * (f - 1), ks, lane);
+  };
+  // the 6 (NP = 3) or 1 MFMAs of output block i as a flat list, MFMA q of block i
+  auto mfma_q = [&](int i, int q, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+    if constexpr (NP == 3) {
+      if (q == 0) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], acs[i], 0, 0, 0);
+      if (q == 1) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], acs[i], 0, 0, 0);
+      if (q == 2) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], acs[i], 0, 0, 0);
+      if (q == 3) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], acs[i], 0, 0, 0);
+      if (q == 4) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], acs[i], 0, 0, 0);
+    }
+    if (q == (NP == 3 ? 5 : 0))
+      acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
+  };
+
   bf16x8 fa[2][NP][TM], fb[2][NP];
   // glds of the next-but-one tile are spread over the first KS-1 k-steps
   constexpr int GSEG = KS - 1;
@@ -346,6 +373,56 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
     });
   };
 
+  // SCH = 1 k-tile: per k-step, wait own reads | (last step: vmcnt, barrier) |
+  // MFMA q, then read groups / glds in its gap, in pinned program order
+  constexpr int NRG = NP * (TM + 1);       // read groups per k-step
+  constexpr int NMF = TM * (NP == 3 ? 6 : 1);  // MFMAs per k-step
+  auto tile_il = [&](int t, auto stage_c, auto next_c) {
+    constexpr bool STAGE_NEXT2 = decltype(stage_c)::value;
+    constexpr bool HAS_NEXT = decltype(next_c)::value;
+    const char* base = lds + (t % HG_STAGES) * C::STAGE;
+    const int sbuf = (t + 2) % HG_STAGES;
+    static_for<KS>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      auto& av = fa[ks & 1];
+      auto& bv = fb[ks & 1];
+      constexpr bool RD = ks + 1 < KS || HAS_NEXT;  // reads to issue in this step
+      const char* rbase = ks + 1 < KS ? base : lds + ((t + 1) % HG_STAGES) * C::STAGE;
+      constexpr int rks = ks + 1 < KS ? ks + 1 : 0;
+      auto& nav = fa[(ks + 1) & 1];
+      auto& nbv = fb[(ks + 1) & 1];
+      hg_wait<0, NP, TM>(av, bv);
+      if constexpr (ks + 1 == KS && HAS_NEXT) {
+        if constexpr (STAGE_NEXT2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // glds of this step (tile t+2), placed after the reads
+      constexpr bool GL = STAGE_NEXT2 && ks < GSEG;
+      constexpr int glo = GL ? ks * C::G / GSEG : 0, ghi = GL ? (ks + 1) * C::G / GSEG : 0;
+      static_for<NMF>([&](auto q_c) {
+        constexpr int q = decltype(q_c)::value;
+        mfma_q(q / (NP == 3 ? 6 : 1), q % (NP == 3 ? 6 : 1), av, bv);
+        if constexpr (RD) {
+          // two read groups per gap from the first gap on
+          if constexpr (2 * q < NRG) read_one(rbase, rks, 2 * q, nav, nbv);
+          if constexpr (2 * q + 1 < NRG) read_one(rbase, rks, 2 * q + 1, nav, nbv);
+        }
+        // then one glds per gap
+        constexpr int g0 = (NRG + 1) / 2;  // first gap without reads
+        if constexpr (q >= g0 && q - g0 < ghi - glo) piece(t + 2, sbuf, glo + q - g0);
+        if constexpr (q == NMF - 1 && ghi - glo > NMF - g0) {
+          for (int r = glo + NMF - g0; r < ghi; ++r) piece(t + 2, sbuf, r);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  };
+
   if (nk > 0) {
     stage(0, 0);
     if (nk > 1) {
@@ -361,9 +438,15 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
     using T_ = std::true_type;
     using F_ = std::false_type;
     int t = 0;
-    for (; t + 2 < nk; ++t) tile(t, T_{}, T_{});
-    if (t + 1 < nk) tile(t++, F_{}, T_{});
-    tile(t, F_{}, F_{});
+    if constexpr (SCH == 1) {
+      for (; t + 2 < nk; ++t) tile_il(t, T_{}, T_{});
+      if (t + 1 < nk) tile_il(t++, F_{}, T_{});
+      tile_il(t, F_{}, F_{});
+    } else {
+      for (; t + 2 < nk; ++t) tile(t, T_{}, T_{});
+      if (t + 1 < nk) tile(t++, F_{}, T_{});
+      tile(t, F_{}, F_{});
+    }
   }
   if constexpr (NP == 3) {
 #pragma unroll
@@ -389,7 +472,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
 // (three buffers: t+1 being read, t+2 in flight, t+3 issued), interleaved with
 // the MFMAs of that last k-step.  The accumulators are repacked into the 32x32
 // register layout of gemm_epilogue<..., 16> (see acc_row / acc_col there).
-template <int AL, int BL, int NP, int BM, int BK>
+// SCH = 1: as gemm_h_kernel's SCH = 1, the next step's fragment reads (and
+// the tile-(t+3) glds) go into the gaps of this step's MFMAs.
+template <int AL, int BL, int NP, int BM, int BK, int SCH = 0>
 __global__ __launch_bounds__(HG_NT, 1) void gemm_h16_kernel(GemmHArgs g) {
   using C = HgCfg<BM, BK, NP>;
   constexpr int TM = BM / 64;        // 32-row blocks per wave (epilogue layout)
@@ -486,6 +571,15 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h16_kernel(GemmHArgs g) {
       }
   };
 
+  // SCH = 1 pieces: read group j (B fragments first, then A), MFMA q = (i, j)
+  auto read_one = [&](const char* base, int ks, int j, bf16x8 (&av)[NP][TA],
+                      bf16x8 (&bv)[NP][TB]) {
+    if (j < TB)
+      bv[0][j] = hg_frag16<BL, BK>(base + NP * C::A_BYTES, wn * 32 + 16 * j, ks, lane);
+    else
+      av[0][j - TB] = hg_frag16<AL, BK>(base, wm * (BM / 2) + 16 * (j - TB), ks, lane);
+  };
+
   bf16x8 fa[2][NP][TA], fb[2][NP][TB];
   constexpr int NM = TA * TB * (NP == 3 ? 6 : 1);  // MFMAs per k-step
   // one k-tile whose first k-step uses register set P0; STAGE3: stage tile
@@ -526,17 +620,65 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h16_kernel(GemmHArgs g) {
       __builtin_amdgcn_sched_barrier(0);
     });
   };
+  constexpr int NRG = TA + TB;  // read groups per k-step (NP = 1)
+  auto tile_il = [&](int t, auto p0_c, auto stage_c, auto next_c, auto g2_c) {
+    constexpr int P0 = decltype(p0_c)::value;
+    constexpr bool STAGE3 = decltype(stage_c)::value;
+    constexpr bool NEXT = decltype(next_c)::value;
+    constexpr bool G2 = decltype(g2_c)::value;
+    const char* base = lds + (t % HG_STAGES) * C::STAGE;
+    static_for<KS>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      constexpr int cs = (P0 + ks) & 1, ns = (P0 + ks + 1) & 1;
+      constexpr bool RD = ks + 1 < KS || NEXT;
+      const char* rbase = ks + 1 < KS ? base : lds + ((t + 1) % HG_STAGES) * C::STAGE;
+      constexpr int rks = ks + 1 < KS ? ks + 1 : 0;
+      hg_wait16<NP, TA, TB>(fa[cs], fb[cs]);
+      if constexpr (ks + 1 == KS && NEXT) {
+        if constexpr (G2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int NG = (ks + 1 == KS && STAGE3) ? C::G : 0;
+      constexpr int g0 = (NRG + 1) / 2;  // first MFMA gap without reads
+      static_for<NM>([&](auto q_c) {
+        constexpr int q = decltype(q_c)::value;
+        constexpr int i = q / TB, j = q % TB;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cs][0][i], fb[cs][0][j], acc[i][j],
+                                                           0, 0, 0);
+        if constexpr (RD) {
+          if constexpr (2 * q < NRG) read_one(rbase, rks, 2 * q, fa[ns], fb[ns]);
+          if constexpr (2 * q + 1 < NRG) read_one(rbase, rks, 2 * q + 1, fa[ns], fb[ns]);
+        }
+        if constexpr (q >= g0 && q - g0 < NG) piece(t + 3, t % HG_STAGES, q - g0);
+        if constexpr (q == NM - 1 && NG > NM - g0) {
+          for (int r = NM - g0; r < NG; ++r) piece(t + 3, t % HG_STAGES, r);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  };
   using T_ = std::true_type;
   using F_ = std::false_type;
   // tile t with its register-set parity (KS odd: sets alternate per tile)
   auto run = [&](int t, auto stage_c, auto next_c, auto g2_c) {
+    auto go = [&](auto p0) {
+      if constexpr (SCH == 1 && NP == 1)
+        tile_il(t, p0, stage_c, next_c, g2_c);
+      else
+        tile(t, p0, stage_c, next_c, g2_c);
+    };
     if constexpr (KS % 2 == 0) {
-      tile(t, std::integral_constant<int, 0>{}, stage_c, next_c, g2_c);
+      go(std::integral_constant<int, 0>{});
     } else {
       if (t & 1)
-        tile(t, std::integral_constant<int, 1>{}, stage_c, next_c, g2_c);
+        go(std::integral_constant<int, 1>{});
       else
-        tile(t, std::integral_constant<int, 0>{}, stage_c, next_c, g2_c);
+        go(std::integral_constant<int, 0>{});
     }
   };
 

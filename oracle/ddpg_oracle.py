@@ -28,11 +28,16 @@ InvertedPendulum/model_ddpg/model-1410.meta -> tests/golden/meta_constants.json)
     beta powers start at b1/b2 and are multiplied by b1/b2 after the update.
   * MSE grad: dQ = -(2*(y-Q)) / B   (Mean_grad 1/B, Square_grad 2x, Sub -1)
 
-Parity status: the TF path cannot be executed here (tensorflow/tflearn/gym
-absent), so this restatement is pinned (a) against an independent torch-fp64
-autograd formulation of the same graph and finite differences (tests), and
-(b) against the reference's own artefacts: trained checkpoints decoded into
-tests/golden/*.npz and the graph constants in meta_constants.json.
+Parity status: TF 1.3 / tflearn / gym are not installed, so the reference's
+own graphs are executed instead: tests/golden/tfgraph.py interprets the
+MetaGraphDefs the reference saved (InvertedPendulum model-1410.meta,
+MountainCar model-120.meta) node by node from their checkpoints, and
+tests/test_graph_pin.py holds this restatement to those trajectories at 1e-6
+(graph_ip1410.npz; graph_ip1410_fresh.npz with the graph's own optimizer
+initializers, i.e. Adam bias correction; graph_mc120.npz with the MountainCar
+widths and a fitted scaler).  Also: an independent torch-fp64 autograd
+formulation and finite differences (tests/test_oracle.py), the decoded
+checkpoints (tests/golden/*.npz) and the graph constants (meta_constants.json).
 """
 import numpy as np
 

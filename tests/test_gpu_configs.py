@@ -265,7 +265,7 @@ def test_c5_bf16_full_dims(dd, O):
     qmax, loss = fl.step(stats=True)
     keys = prof.read()
     prof.enable(False)
-    assert any(k.startswith("gemm_bf16_kernel") or
+    assert any((k.startswith("gemm_s3_kernel") and "NP=1" in k) or
                (k.startswith("gemm_h") and "NP=1" in k) for k in keys), sorted(keys)
     idx = np.array(random.Random(1234).sample(range(6000), B))
     L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)

@@ -445,7 +445,7 @@ def test_bf16_parity_and_kernel_use(dd, O):
         L.step(*(x[idx] for x in rows))
     keys = prof.read()
     prof.enable(False)
-    assert any(k.startswith("gemm_bf16_kernel") or
+    assert any((k.startswith("gemm_s3_kernel") and "NP=1" in k) or
                (k.startswith("gemm_h") and "NP=1" in k) for k in keys), sorted(keys)
     for which, net, names in ((_lib.ACTOR, "actor", O.ACTOR_KEYS),
                               (_lib.CRITIC, "critic", O.CRITIC_KEYS)):

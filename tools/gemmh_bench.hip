@@ -70,10 +70,10 @@ struct Case {
   int al, bl, np, M, N, K, splits;
 };
 
-static float *gA, *gB, *gC, *gR;
-static __bf16 *hA, *hB;
+static float *gA, *gB, *gC, *gR, *gBias;
+static __bf16 *hA, *hB, *gTw;
 
-template <int AL, int BL, int NP, int BM, int BK, int MF>
+template <int AL, int BL, int NP, int BM, int BK, int MF, int SCH = 0>
 static void run_case(const Case& c) {
   const size_t na = (size_t)c.M * c.K, nb = (size_t)c.K * c.N, nc = (size_t)c.M * c.N;
   // fresh operands (NP = 1 rounds them), planes
@@ -120,14 +120,33 @@ static void run_case(const Case& c) {
   g.e.out = gC;
   g.e.ldo = c.N;
   g.e.out_split_stride = (long long)nc;
+  // env GH_EPI (unsplit cases): 1 = fp32 out + bf16 twin (NP planes) + bias + elu
+  // (the learner's forward epilogue), 2 = the twin only + bias + elu
+  const char* ev = getenv("GH_EPI");
+  const int epi = (ev && c.splits == 1) ? atoi(ev) : 0;
+  if (epi) {
+    g.e.bias = gBias;
+    g.e.act = 1;
+    g.e.outh = gTw;
+    g.e.h_plane_stride = (long long)nc;
+    g.e.h_planes = NP;
+    if (epi == 2) g.e.out = nullptr;
+  }
   dim3 grid((c.N + HG_BN - 1) / HG_BN, (c.M + BM - 1) / BM, c.splits);
   auto f = [&] {
     if constexpr (MF == 16)
-      hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, NP, BM, BK>), grid, dim3(HG_NT), 0, 0, g);
+      hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, NP, BM, BK, SCH>), grid, dim3(HG_NT), 0, 0, g);
     else
-      hipLaunchKernelGGL((gemm_h_kernel<AL, BL, NP, BM, BK>), grid, dim3(HG_NT), 0, 0, g);
+      hipLaunchKernelGGL((gemm_h_kernel<AL, BL, NP, BM, BK, SCH>), grid, dim3(HG_NT), 0, 0, g);
   };
   const float us = time_it(f, 10);
+  if (epi) {  // elu'd outputs: timing only
+    printf("%-26s MF%d S%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d EPI%d  %8.2f us %7.1f TF\n", c.name,
+           MF, SCH, NP, BM, BK, c.M, c.N, c.K, c.splits, epi, us,
+           2.0 * c.M * c.N * (double)c.K / (us * 1e-6) / 1e12);
+    fflush(stdout);
+    return;
+  }
   // check: sum the split slabs on the host
   std::vector<float> out(nc * c.splits), ref(nc);
   CHECK(hipMemcpy(out.data(), gC, nc * c.splits * 4, hipMemcpyDeviceToHost));
@@ -162,24 +181,31 @@ static void run_case(const Case& c) {
   const double flop = 2.0 * c.M * c.N * (double)c.K;
   const double tf = flop / (us * 1e-6) / 1e12;
   const double peak = NP == 3 ? 2500.0 / 6 : 2500.0;
-  printf("%-26s MF%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d  %8.2f us %7.1f TF (%5.1f%% of %.0f)  "
-         "vs f32 %.2e | vs f64: gemm_h %.2e, f32 MFMA %.2e\n",
-         c.name, MF, NP, BM, BK, c.M, c.N, c.K, c.splits, us, tf, 100.0 * tf / peak, peak,
-         maxerr / maxref, e64h / m64, e64r / m64);
+  printf("%-26s MF%d S%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d  %8.2f us %7.1f TF (%5.1f%% of %.0f)  "
+         "vs f32 %.2e | vs f64: gemm_h %.2e, f32 MFMA %.2e | out %.9e\n",
+         c.name, MF, SCH, NP, BM, BK, c.M, c.N, c.K, c.splits, us, tf, 100.0 * tf / peak, peak,
+         maxerr / maxref, e64h / m64, e64r / m64, (double)out[nc / 3 + 7]);
   fflush(stdout);
 }
 
-template <int NP, int BM, int BK, int MF>
+template <int NP, int BM, int BK, int MF, int SCH = 0>
 static void dispatch1(const Case& c) {
-  if (c.al == L_RK && c.bl == L_KR) run_case<L_RK, L_KR, NP, BM, BK, MF>(c);
-  if (c.al == L_RK && c.bl == L_RK) run_case<L_RK, L_RK, NP, BM, BK, MF>(c);
-  if (c.al == L_KR && c.bl == L_KR) run_case<L_KR, L_KR, NP, BM, BK, MF>(c);
+  if (c.al == L_RK && c.bl == L_KR) run_case<L_RK, L_KR, NP, BM, BK, MF, SCH>(c);
+  if (c.al == L_RK && c.bl == L_RK) run_case<L_RK, L_RK, NP, BM, BK, MF, SCH>(c);
+  if (c.al == L_KR && c.bl == L_KR) run_case<L_KR, L_KR, NP, BM, BK, MF, SCH>(c);
 }
-// the 32x32x16 and the 16x16x32 kernel on the same case, interleaved
+// the 32x32x16 kernel (both schedules) and the 16x16x32 kernel on the same
+// case, interleaved
 template <int NP, int BM, int BK>
 static void dispatch(const Case& c) {
-  dispatch1<NP, BM, BK, 32>(c);
-  if constexpr (NP == 1) dispatch1<NP, BM, BK, 16>(c);
+  for (int rep = 0; rep < 2; ++rep) {
+    dispatch1<NP, BM, BK, 32, 0>(c);
+    dispatch1<NP, BM, BK, 32, 1>(c);
+    if constexpr (NP == 1) {
+      dispatch1<NP, BM, BK, 16, 0>(c);
+      dispatch1<NP, BM, BK, 16, 1>(c);
+    }
+  }
 }
 
 int main(int argc, char** argv) {
@@ -191,8 +217,12 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&gR, maxe * 4));
   CHECK(hipMalloc(&hA, maxe * 2 * 3));
   CHECK(hipMalloc(&hB, maxe * 2 * 3));
+  CHECK(hipMalloc(&gTw, maxe * 2 * 3));
+  CHECK(hipMalloc(&gBias, 4096 * 4));
+  CHECK(hipMemset(gBias, 0, 4096 * 4));
   const Case cases[] = {
       // C5 (bf16): forward, dX, weight gradients
+      {"c5 first fwd <RK,KR>", L_RK, L_KR, 1, 4096, 2048, 384, 1},
       {"c5 fwd <RK,KR>", L_RK, L_KR, 1, 4096, 2048, 2048, 1},
       {"c5 fwd <RK,KR>", L_RK, L_KR, 1, 4096, 2048, 4096, 1},
       {"c5 dx <RK,RK>", L_RK, L_RK, 1, 4096, 4096, 2048, 1},
@@ -212,14 +242,25 @@ int main(int argc, char** argv) {
       {"c3 thin wgrad <KR,KR>", L_KR, L_KR, 3, 64, 1024, 4096, 16},
       {"c3 thin wgrad <KR,KR>", L_KR, L_KR, 3, 64, 1024, 4096, 32},
   };
+  // env GH_TILES=1: the bf16 cases on the 16x16x32 kernel at every (BM, BK)
+  const bool tiles = getenv("GH_TILES") && atoi(getenv("GH_TILES"));
   for (const Case& c : cases) {
     char full[96];
     snprintf(full, sizeof full, "%s M=%d N=%d K=%d", c.name, c.M, c.N, c.K);
     if (only && !strstr(full, only)) continue;
-    if (c.np == 1)
+    if (c.np == 1 && tiles) {
+      for (int rep = 0; rep < 2; ++rep) {
+        // (BK = 32 builds of the 16x16x32 kernel fail tools/isa_check.py:
+        // with one k-step per tile the register sets alternate by tile parity
+        // and hipcc copies in-flight fragment registers -- never run them)
+        dispatch1<1, 256, 64, 16>(c);
+        dispatch1<1, 128, 64, 16>(c);
+      }
+    } else if (c.np == 1) {
       dispatch<1, 256, 64>(c);
-    else
+    } else {
       dispatch<3, 128, 32>(c);
+    }
   }
   printf("done\n");
   return 0;
