@@ -19,6 +19,7 @@
 #include "gemm_s3.h"
 #include "gemm_h.h"
 #include "thin_k.h"
+#include "skinny.h"
 #include "kernels.h"
 #include "sampler.h"
 #include "small_batch.h"
@@ -235,6 +236,7 @@ struct ddpg_ctx {
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
+    bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
   } sw;
 
   // comm: every collective of the ctx is issued on cs (one stream, so the
@@ -874,6 +876,69 @@ static void critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int 
   HIP_TRY(hipGetLastError());
 }
 
+// Weight gradient dW[M][N] = A^T . B over K = B rows (A [K][lda] M columns,
+// B [K][ldb] N columns; split-K slabs [split][M][N] or `direct`): on the
+// skinny kernel (skinny.h) when one side is at most 64 wide and the other a
+// multiple of 4 (>= 128), with the narrow operand's row holding every column
+// its NG-wide tiles read; otherwise on the GEMMs.
+static GemmPlan wgrad_launch(ddpg_ctx* c, const float* A, int lda, const float* B, int ldb, int M,
+                             int N, int K, float* slab, int cap, float* direct) {
+  const bool a_narrow = M <= SK_NMAX && N >= 128;
+  const bool b_narrow = N <= SK_NMAX && M >= 128 && !a_narrow;
+  const float* nar = a_narrow ? A : B;
+  const int ldn = a_narrow ? lda : ldb, nn = a_narrow ? M : N;
+  const int ldw = a_narrow ? ldb : lda, nw = a_narrow ? N : M;
+  // 16 narrow columns per wave above 16 (one 128 KB reduction: 1 block per
+  // CU, 256 blocks); 8 at or below (64 KB, 2 blocks per CU, 512 blocks) --
+  // measured, profiles/r3/skinny_variants.txt
+  const int ng = (nn > 16 && rup(nn, 16) <= ldn) ? 16 : 8;
+  const int ntn = ceil_div(std::max(nn, 1), ng);
+  if (c->sw.skinny && (a_narrow || b_narrow) && nw % 4 == 0 && ldw % 4 == 0 &&
+      ntn * ng <= ldn && aligned16(a_narrow ? B : A)) {
+    GemmPlan p;
+    const int ntw = ceil_div(nw, SK_WT), tiles = ntw * ntn;
+    int splits = std::min(cap, std::max(1, (ng == 8 ? 512 : 256) / tiles));
+    int kc = rup(ceil_div(K, splits), SK_WAVES);
+    splits = ceil_div(K, kc);
+    p.splits = splits;
+    SkArgs a;
+    a.N = nar;
+    a.ldn = ldn;
+    a.nn = nn;
+    a.W = a_narrow ? B : A;
+    a.ldw = ldw;
+    a.nw = nw;
+    a.B = K;
+    a.kc = kc;
+    a.ntw = ntw;
+    a.ntn = ntn;
+    a.narrow_rows = a_narrow ? 1 : 0;
+    if (splits == 1 && direct) {
+      a.out = direct;
+      a.split_stride = 0;
+      p.direct = true;
+    } else {
+      a.out = slab;
+      a.split_stride = (long long)M * N;
+    }
+    ProfScope ps(c, "skinny_wgrad_kernel|wgrad", 2.0 * M * N * (double)K,
+                 4.0 * ((double)K * (M + N) + (double)M * N * splits));
+    if (ng == 8)
+      hipLaunchKernelGGL(skinny_wgrad_kernel<8>, dim3(tiles * splits), dim3(SK_NT),
+                         sk_lds_bytes(8), c->cur, a);
+    else
+      hipLaunchKernelGGL(skinny_wgrad_kernel<16>, dim3(tiles * splits), dim3(SK_NT),
+                         sk_lds_bytes(16), c->cur, a);
+    HIP_TRY(hipGetLastError());
+    return p;
+  }
+  GemmEpi e = epi_none();
+  e.out = slab;
+  e.ldo = N;
+  e.out_split_stride = (long long)M * N;
+  return gemm_launch<L_KR, L_KR>(c, "wgrad", A, lda, B, ldb, M, N, K, e, 0, cap, direct);
+}
+
 static void add_seg(ReduceTable& t, const float* src, float* dst, long long stride, int nslab,
                     long long count) {
   ReduceSeg& s = t.seg[t.nseg++];
@@ -1084,17 +1149,10 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
                                          c->CH2, B, 2 * c->CH1, c->CH2, e);
   const int mt = pdc.mt(B);
   // dWs = s^T . dcs ; dWa = a^T . dca
-  e = epi_none();
-  e.out = c->slab_Ws;
-  e.ldo = c->CH1;
-  e.out_split_stride = (long long)c->S * c->CH1;
-  GemmPlan pWs = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1,
-                                         B, e, 0, c->split_cap_Ws, c->grad + L.c[CWS].off);
-  e.out = c->slab_Wa;
-  e.out_split_stride = (long long)c->A * c->CH1;
-  GemmPlan pWa = gemm_launch<L_KR, L_KR>(c, "wgrad", c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A,
-                                         c->CH1, B, e, 0, c->split_cap_Wa,
-                                         c->grad + L.c[CWA].off);
+  GemmPlan pWs = wgrad_launch(c, c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, c->slab_Ws,
+                              c->split_cap_Ws, c->grad + L.c[CWS].off);
+  GemmPlan pWa = wgrad_launch(c, c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A, c->CH1, B,
+                              c->slab_Wa, c->split_cap_Wa, c->grad + L.c[CWA].off);
   if (par) fork_to(c, 5, c->aux[0], main);  // join dWh
   // gather every critic gradient into the flat grad buffer
   ReduceTable tab;
@@ -1131,12 +1189,9 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
     fork_to(c, 6, main, c->aux[0]);
     c->cur = c->aux[0];
   }
+  GemmPlan pW3 = wgrad_launch(c, c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, c->slab_W3,
+                              c->split_cap_W3, G + L.a[AW3].off);
   GemmEpi e = epi_none();
-  e.out = c->slab_W3;
-  e.ldo = c->A;
-  e.out_split_stride = (long long)c->AH2 * c->A;
-  GemmPlan pW3 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A,
-                                         B, e, 0, c->split_cap_W3, G + L.a[AW3].off);
   c->cur = main;
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
   // dz2 feeds dW2 and dz1 only; dz1 feeds dW1 only: twin-only when those run
@@ -1216,12 +1271,8 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   GemmPlan pz1 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz2, c->ldAH2, P(c, c->theta, L.a[AW2]),
                                          c->AH2, B, c->AH1, c->AH2, e);
   // dW1 = s^T . dz1
-  e = epi_none();
-  e.out = c->slab_W1;
-  e.ldo = c->AH1;
-  e.out_split_stride = (long long)c->S * c->AH1;
-  GemmPlan pW1 = gemm_launch<L_KR, L_KR>(c, "wgrad", c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1,
-                                         B, e, 0, c->split_cap_W1, G + L.a[AW1].off);
+  GemmPlan pW1 = wgrad_launch(c, c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1, B, c->slab_W1,
+                              c->split_cap_W1, G + L.a[AW1].off);
   if (par) fork_to(c, 3, c->aux[0], main);  // join dW3, dW2
   ReduceTable tab;
   tab.nseg = 0;
@@ -1630,6 +1681,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
+      c->sw.skinny = !env_is("DDPG_SKINNY", "0");
     }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;
@@ -1816,6 +1868,10 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
           }
       }
     }
+    HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, sk_lds_bytes(8)));
+    HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<16>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, sk_lds_bytes(16)));
     HIP_TRY(hipDeviceSynchronize());
   });
   if (rc != DDPG_OK) {

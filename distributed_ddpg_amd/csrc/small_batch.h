@@ -183,78 +183,29 @@ SB_FN void sb_fma4(f32x4 (&acc)[4], f32x4 x, f32x4 w) {
   }
 }
 
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
-// not for its global loads (__syncthreads' fence waits vmcnt(0), which would
-// drain the next level's weight prefetch at every barrier).  Every cross-
-// thread hand-off inside a phase kernel goes through LDS; the global stores
-// (saves, stats) are read only by later launches.
-SB_FN void sb_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// A thread's first batch of weight quads for the NEXT dense layer, loaded
-// while the current level finishes (its reduction, epilogue and barriers):
-// the weights do not depend on the activations, so the first load round trip
-// of every dense level leaves the level's dependent chain.
-struct SbPre {
-  f32x4 w[SB_U];
-};
-
 // Dense layer, part 1 on threads t < nt of a wave-aligned group: thread t owns
 // column quad q = t % NQ of k-slice s = t / NQ (S = min(nt / NQ, K) slices)
 // and the k rows s, s + S, ...; the SB_U loads of a batch are all issued
-// before any is consumed (the first batch may come prefetched, `pre`).
-// Partials go to red[s][n][r] (f32x4 per n).
-struct SbDenseMap {
-  int S, q, s, nk;
-  const glb_v4* wp;
-  size_t step;
-};
-SB_FN SbDenseMap sb_dense_map(const SbOp& o, int t, int nt) {
-  SbDenseMap m;
+// before any is consumed.  Partials go to red[s][n][r] (f32x4 per n).
+SB_FN void sb_dense_part(const SbOp& o, int t, int nt, lds_f* red) {
   const int NQ = o.N >> 2;
-  m.S = min(nt / NQ, o.K);
-  m.q = t % NQ;
-  m.s = t / NQ;
-  m.step = (size_t)m.S * (o.ldw >> 2);  // float4s between this thread's k rows
-  m.wp = reinterpret_cast<const glb_v4*>(o.W) + m.q + (size_t)m.s * (o.ldw >> 2);
-  m.nk = m.s < m.S ? (o.K - m.s + m.S - 1) / m.S : 0;  // this thread's k rows
-  return m;
-}
-// the first batch as sb_dense_part loads it (clamped to the thread's rows)
-#ifndef SB_PREFETCH
-#define SB_PREFETCH 1  // 0: no cross-level weight prefetch (A/B builds)
-#endif
-SB_FN void sb_dense_prefetch(const SbOp& o, int t, int nt, SbPre& pre) {
-  if (!SB_PREFETCH) return;
-  const SbDenseMap m = sb_dense_map(o, t, nt);
-  if (m.nk == 0) return;
-#pragma unroll
-  for (int u = 0; u < SB_U; ++u) pre.w[u] = m.wp[min(u, m.nk - 1) * m.step];
-}
-template <bool PRE = false>
-SB_FN void sb_dense_part(const SbOp& o, int t, int nt, lds_f* red, const SbPre& pre) {
-  const SbDenseMap m = sb_dense_map(o, t, nt);
-  if (m.nk == 0) return;
-  const int S = m.S, s = m.s, q = m.q, nk = m.nk;
-  const size_t step = m.step;
-  const glb_v4* wp = m.wp;
+  const int S = min(nt / NQ, o.K);
+  const int q = t % NQ, s = t / NQ;
+  if (s >= S) return;
   f32x4 acc[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int K = o.K;
   const lds_v4* X4 = reinterpret_cast<const lds_v4*>(o.X);
+  const glb_v4* Wq = reinterpret_cast<const glb_v4*>(o.W) + q;
+  const size_t step = (size_t)S * (o.ldw >> 2);  // float4s between this thread's k rows
+  const glb_v4* wp = Wq + (size_t)s * (o.ldw >> 2);
+  const int nk = (K - s + S - 1) / S;  // this thread's k rows
   int i = 0;
   for (; i + SB_U <= nk; i += SB_U) {
     f32x4 w[SB_U];
-    if (PRE && i == 0) {
 #pragma unroll
-      for (int u = 0; u < SB_U; ++u) w[u] = pre.w[u];
-    } else {
-#pragma unroll
-      for (int u = 0; u < SB_U; ++u) w[u] = wp[u * step];
-    }
+    for (int u = 0; u < SB_U; ++u) w[u] = wp[u * step];
 #pragma unroll
     for (int u = 0; u < SB_U; ++u) sb_fma4(acc, X4[s + (i + u) * S], w[u]);
     wp += SB_U * step;
@@ -262,13 +213,8 @@ SB_FN void sb_dense_part(const SbOp& o, int t, int nt, lds_f* red, const SbPre& 
   if (i < nk) {  // remainder: clamped loads, masked FMAs
     f32x4 w[SB_U];
     const int rem = nk - i;
-    if (PRE && i == 0) {
 #pragma unroll
-      for (int u = 0; u < SB_U; ++u) w[u] = pre.w[u];
-    } else {
-#pragma unroll
-      for (int u = 0; u < SB_U; ++u) w[u] = wp[min(u, rem - 1) * step];
-    }
+    for (int u = 0; u < SB_U; ++u) w[u] = wp[min(u, rem - 1) * step];
 #pragma unroll
     for (int u = 0; u < SB_U; ++u)
       if (u < rem) sb_fma4(acc, X4[s + (i + u) * S], w[u]);
@@ -361,23 +307,7 @@ SB_FN void sb_thin_epi(const SbOp& o, int t, int nt, const lds_f* red) {
 // the weights', and parked in LDS for the epilogue).  Ends with a barrier.
 constexpr int SB_BIAS = 2048;  // LDS floats for biases (+ as many for pw)
 template <int NOPS>
-SB_FN void sb_prefetch(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], SbPre& pre) {
-  constexpr int nt = SB_NT / NOPS;
-  const int grp = threadIdx.x / nt, t = threadIdx.x - grp * nt;
-#pragma unroll
-  for (int i = 0; i < NOPS; ++i)
-    if (grp == i && !thin[i]) sb_dense_prefetch(ops[i], t, nt, pre);
-}
-struct SbNoNext {
-  SB_FN void operator()() const {}
-};
-
-// pre: this level's prefetched first weight batches (from sb_prefetch over
-// the same ops); next(): issues the next level's prefetch, called once this
-// level's partials are written, before its barriers.
-template <int NOPS, bool PRE = false, class Next = SbNoNext>
-SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* red,
-                    const SbPre& pre, Next next = Next()) {
+SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* red) {
   constexpr int nt = SB_NT / NOPS;
   constexpr int rs = SB_RED / NOPS;
   constexpr int bs = SB_BIAS / NOPS;
@@ -398,7 +328,7 @@ SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* re
           bv[j] = (hb && n < o.N) ? o.b[n] : 0.f;
           pv[j] = (o.epi == SB_POST2 && n < o.N) ? o.pw[n] : 0.f;
         }
-        sb_dense_part<PRE && SB_PREFETCH>(o, t, nt, red + i * rs, pre);
+        sb_dense_part(o, t, nt, red + i * rs);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int n = t + j * nt;
@@ -409,40 +339,20 @@ SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* re
         }
       }
     }
-  next();
-  sb_sync();
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < NOPS; ++i)
     if (grp == i) {
       if (thin[i]) sb_thin_epi(ops[i], t, nt, red + i * rs);
       else sb_dense_epi(ops[i], t, nt, red + i * rs, bias + i * bs, bias + SB_BIAS + i * bs);
     }
-  sb_sync();
+  __syncthreads();
 }
 
-// a level without prefetch in or out
-template <int NOPS>
-SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* red) {
-  SbPre none;
-  sb_level<NOPS, false>(ops, thin, red, none);
-}
 SB_FN void sb_dense1(const SbOp& o, lds_f* red) {
   const SbOp ops[1] = {o};
   const bool th[1] = {false};
   sb_level<1>(ops, th, red);
-}
-// a single dense layer as a level whose first weight batch was prefetched
-// into `pre`; next() prefetches the following dense level
-template <class Next = SbNoNext>
-SB_FN void sb_dense1p(const SbOp& o, lds_f* red, const SbPre& pre, Next next = Next()) {
-  const SbOp ops[1] = {o};
-  const bool th[1] = {false};
-  sb_level<1, true>(ops, th, red, pre, next);
-}
-SB_FN void sb_prefetch1(const SbOp& o, SbPre& pre) {
-  const SbOp ops[1] = {o};
-  const bool th[1] = {false};
-  sb_prefetch<1>(ops, th, pre);
 }
 
 SB_FN void sb_thin1(SbOp o, bool trans, bool act_tanh, lds_f* red) {
@@ -492,23 +402,6 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   const glb_f* P = GLB(g.theta);
   SB_STAMP(0);
 
-  // the levels' ops (pointer bundles; built up front so that each level can
-  // prefetch the next dense level's first weight batch)
-  const SbOp ops1[4] = {sb_op(xs2, g.S, T + g.aW1, g.AH1, g.AH1, T + g.ab1, SB_ELU, b1),
-                        sb_op(xs2, g.S, T + g.cWs, g.CH1, g.CH1, T + g.cbs, SB_ELU, b3),
-                        sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat),
-                        sb_op(xa, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU,
-                              cat + 4 * g.CH1)};
-  const bool th1[4] = {false, false, false, false};
-  const SbOp ops2[2] = {sb_op(b1, g.AH1, T + g.aW2, g.AH2, g.AH2, T + g.ab2, SB_ELU, b2),
-                        sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_ELU, h)};
-  const bool th2[2] = {false, false};
-  const SbOp op4 = sb_op(ta2, g.A, T + g.cWa, g.CH1, g.CH1, T + g.cba, SB_ELU, b3 + 4 * g.CH1);
-  const SbOp op5 = sb_op(b3, 2 * g.CH1, T + g.cWh, g.CH2, g.CH2, T + g.cbh, SB_ELU, b1);
-  const SbOp op7 = sb_op(b2, g.CH2, GLB(g.whT), 2 * g.CH1, 2 * g.CH1, nullptr, SB_AUX, b3, cat);
-  SbPre pf0, pf1;
-  sb_prefetch<4>(ops1, th1, pf0);  // in flight under the row gather
-
   if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw + 2, g.alpha + 1, g.lr_c, g.b1, g.b2);
   // rows -> xs / xs2 / xa ([feature][4], zero past S / A and for rows past
   // `valid`) in one pass: one slot read, then every ring read of an element in
@@ -544,13 +437,24 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
     col[4 * 4 + tid] = ok ? (g.rrd ? (float)g.rrd[sl] : g.rr[sl]) : 0.f;
     col[5 * 4 + tid] = ok ? g.rt[sl] : 0.f;
   }
-  sb_sync();
+  __syncthreads();
   SB_STAMP(1);
-  // L1: target h1 | target state branch | online state branch | online action branch
-  sb_level<4, true>(ops1, th1, red, pf0, [&] { sb_prefetch<2>(ops2, th2, pf1); });
+  {  // L1: target h1 | target state branch | online state branch | online action branch
+    const SbOp ops[4] = {sb_op(xs2, g.S, T + g.aW1, g.AH1, g.AH1, T + g.ab1, SB_ELU, b1),
+                         sb_op(xs2, g.S, T + g.cWs, g.CH1, g.CH1, T + g.cbs, SB_ELU, b3),
+                         sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat),
+                         sb_op(xa, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU,
+                               cat + 4 * g.CH1)};
+    const bool th[4] = {false, false, false, false};
+    sb_level<4>(ops, th, red);
+  }
   SB_STAMP(2);
-  // L2: target h2 | online critic hidden (networks.py:154-156); L4's weights next
-  sb_level<2, true>(ops2, th2, red, pf1, [&] { sb_prefetch1(op4, pf0); });
+  {  // L2: target h2 | online critic hidden (networks.py:154-156)
+    const SbOp ops[2] = {sb_op(b1, g.AH1, T + g.aW2, g.AH2, g.AH2, T + g.ab2, SB_ELU, b2),
+                         sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_ELU, h)};
+    const bool th[2] = {false, false};
+    sb_level<2>(ops, th, red);
+  }
   SB_STAMP(3);
   {  // L3: target actor out o' = tanh(h2' W3') | online q = h Wo + bo
     SbOp ops[2] = {sb_op(b2, g.AH2, T + g.aW3, g.A, g.A, nullptr, SB_NONE, ta2),
@@ -560,12 +464,12 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
     sb_level<2>(ops, th, red);
   }
   for (int idx = tid; idx < 4 * g.A; idx += SB_NT) ta2[idx] = __fmul_rn(ta2[idx], g.scale);
-  sb_sync();
+  __syncthreads();
   SB_STAMP(4);
   // L4: target action branch; L5: target critic hidden; L6: q'
-  sb_dense1p(op4, red, pf0, [&] { sb_prefetch1(op5, pf1); });
+  sb_dense1(sb_op(ta2, g.A, T + g.cWa, g.CH1, g.CH1, T + g.cba, SB_ELU, b3 + 4 * g.CH1), red);
   SB_STAMP(5);
-  sb_dense1p(op5, red, pf1, [&] { sb_prefetch1(op7, pf0); });
+  sb_dense1(sb_op(b3, 2 * g.CH1, T + g.cWh, g.CH2, g.CH2, T + g.cbh, SB_ELU, b1), red);
   SB_STAMP(6);
   sb_thin1(sb_op(b1, g.CH2, T + g.cWo, 1, 1, T + g.cbo, SB_NONE, col), false, false, red);
   SB_STAMP(7);
@@ -590,23 +494,23 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
     g.stat_part[wg * 2 + 0] = lsum;
     g.stat_part[wg * 2 + 1] = qmax;
   }
-  sb_sync();
+  __syncthreads();
   // ---- critic head backward: dhp = dq * Wo * elu'(h) -> b2
   for (int idx = tid; idx < 4 * g.CH2; idx += SB_NT) {
     const int j = idx >> 2, r = idx & 3;
     b2[idx] = __fmul_rn(__fmul_rn(col[3 * 4 + r], P[g.cWo + j]), elu_grad_factor(h[idx]));
   }
-  sb_sync();
+  __syncthreads();
   SB_STAMP(8);
   // L7: dcat = dhp . Wh^T * elu'(cat) -> b3   (Wh^T read from its row-major shadow)
-  sb_dense1p(op7, red, pf0);
+  sb_dense1(sb_op(b2, g.CH2, GLB(g.whT), 2 * g.CH1, 2 * g.CH1, nullptr, SB_AUX, b3, cat), red);
   SB_STAMP(9);
   sb_save(g.sv.cat, g.sv.Bp, 2 * g.CH1, cat, r0);
   sb_save(g.sv.dcat, g.sv.Bp, 2 * g.CH1, b3, r0);
   sb_save(g.sv.h, g.sv.Bp, g.CH2, h, r0);
   sb_save(g.sv.dhp, g.sv.Bp, g.CH2, b2, r0);
   if (g.stamps) {
-    sb_sync();
+    __syncthreads();
     SB_STAMP(10);
   }
 }
@@ -631,43 +535,38 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   const glb_f* P = GLB(g.theta);
   SB_STAMP(32);
 
-  const SbOp ops1[2] = {sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1),
-                        sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat)};
-  const bool th1[2] = {false, false};
-  const SbOp op2 = sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2);
-  const SbOp op4 = sb_op(mu, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, cat + 4 * g.CH1);
-  const SbOp op5 = sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_POST2, dh,
-                         nullptr, P + g.cWo);
-  const SbOp op6 = sb_op(dh, g.CH2, GLB(g.whT) + g.CH1, 2 * g.CH1, g.CH1, nullptr, SB_AUX,
-                         cat + 4 * g.CH1, cat + 4 * g.CH1);
-  const SbOp op8 = sb_op(dh, g.AH2, GLB(g.w2T), g.AH1, g.AH1, nullptr, SB_AUX, cat, h1);
-  SbPre pf0, pf1;
-  sb_prefetch<2>(ops1, th1, pf0);
-
   if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw, g.alpha, g.lr_a, g.b1, g.b2);
   for (int idx = tid; idx < 4 * LX; idx += SB_NT) {  // phase 1 saved the (scaled) rows
     const int k = idx >> 2, r = idx & 3;
     xs[idx] = (r < valid && k < g.S) ? g.sv.xs[(size_t)k * g.sv.Bp + r0 + r] : 0.f;
   }
-  sb_sync();
+  __syncthreads();
   SB_STAMP(33);
-  // L1: actor h1 | critic state branch
-  sb_level<2, true>(ops1, th1, red, pf0, [&] { sb_prefetch1(op2, pf1); });
+  {  // L1: actor h1 | critic state branch
+    const SbOp ops[2] = {sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1),
+                         sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat)};
+    const bool th[2] = {false, false};
+    sb_level<2>(ops, th, red);
+  }
   SB_STAMP(34);
   // L2: h2; L3: o = tanh(h2 W3), mu = scale o   (networks.py:51-63, ddpg.py:106)
-  sb_dense1p(op2, red, pf1, [&] { sb_prefetch1(op4, pf0); });
+  sb_dense1(sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2), red);
   SB_STAMP(35);
   sb_thin1(sb_op(h2, g.AH2, P + g.aW3, g.A, g.A, nullptr, SB_NONE, o), false, true, red);
   for (int idx = tid; idx < 4 * g.A; idx += SB_NT) mu[idx] = __fmul_rn(o[idx], g.scale);
-  sb_sync();
+  __syncthreads();
   SB_STAMP(36);
   // L4: action branch at mu; L5: dhp2 = Wo * elu'(h')  (updated critic, grad_ys = 1,
   // networks.py:143); L6: dca = dhp2 . Wh[CH1:]^T * elu'(ca), in place over ca
-  sb_dense1p(op4, red, pf0, [&] { sb_prefetch1(op5, pf1); });
+  sb_dense1(sb_op(mu, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, cat + 4 * g.CH1), red);
   SB_STAMP(37);
-  sb_dense1p(op5, red, pf1, [&] { sb_prefetch1(op6, pf0); });
+  sb_dense1(sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_POST2, dh, nullptr,
+                  P + g.cWo),
+            red);
   SB_STAMP(38);
-  sb_dense1p(op6, red, pf0, [&] { sb_prefetch1(op8, pf1); });
+  sb_dense1(sb_op(dh, g.CH2, GLB(g.whT) + g.CH1, 2 * g.CH1, g.CH1, nullptr, SB_AUX,
+                  cat + 4 * g.CH1, cat + 4 * g.CH1),
+            red);
   SB_STAMP(39);
   // L7: da = dca . Wa^T -> dz3 (scratch), then dz3 = ((-da) * scale) * (1 - o^2), masked
   sb_thin1(sb_op(cat + 4 * g.CH1, g.CH1, P + g.cWa, g.CH1, g.A, nullptr, SB_NONE, dz3), true,
@@ -677,7 +576,7 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
     const float dy = __fmul_rn(-dz3[idx], g.scale);
     dz3[idx] = (idx & 3) < valid ? __fmul_rn(dy, __fsub_rn(1.f, __fmul_rn(ov, ov))) : 0.f;
   }
-  sb_sync();
+  __syncthreads();
   // ---- actor backward (networks.py:44)
   // dz2 = dz3 . W3^T * elu'(h2) -> dh   (K = A is tiny: one thread per output)
   for (int idx = tid; idx < 4 * g.AH2; idx += SB_NT) {
@@ -686,10 +585,10 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
     for (int a = 0; a < g.A; ++a) v = fmaf(dz3[a * 4 + r], P[g.aW3 + (size_t)n * g.A + a], v);
     dh[idx] = __fmul_rn(v, elu_grad_factor(h2[idx]));
   }
-  sb_sync();
+  __syncthreads();
   SB_STAMP(40);
   // L8: dz1 = dz2 . W2^T * elu'(h1) -> cat
-  sb_dense1p(op8, red, pf1);
+  sb_dense1(sb_op(dh, g.AH2, GLB(g.w2T), g.AH1, g.AH1, nullptr, SB_AUX, cat, h1), red);
   SB_STAMP(41);
   sb_save(g.sv.h1, g.sv.Bp, g.AH1, h1, r0);
   sb_save(g.sv.h2, g.sv.Bp, g.AH2, h2, r0);
@@ -697,7 +596,7 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   sb_save(g.sv.dz2, g.sv.Bp, g.AH2, dh, r0);
   sb_save(g.sv.dz3, g.sv.Bp, g.A, dz3, r0);
   if (g.stamps) {
-    sb_sync();
+    __syncthreads();
     SB_STAMP(42);
   }
 }
@@ -724,10 +623,6 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
   lds_f* h1 = o + 4 * LX;  // [LW][4]
   lds_f* h2 = h1 + 4 * LW;
   const glb_f* P = GLB(base);
-  const SbOp op1 = sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1);
-  const SbOp op2 = sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2);
-  SbPre pf0, pf1;
-  sb_prefetch1(op1, pf0);
   for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
     const int k = idx >> 2, r = idx & 3;
     float x = 0.f;
@@ -735,9 +630,9 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
     if (r < valid && k < g.S) x = in.s[(r0 + r) * g.S + k];
     xs[idx] = x;
   }
-  sb_sync();
-  sb_dense1p(op1, red, pf0, [&] { sb_prefetch1(op2, pf1); });
-  sb_dense1p(op2, red, pf1);
+  __syncthreads();
+  sb_dense1(sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1), red);
+  sb_dense1(sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2), red);
   sb_thin1(sb_op(h2, g.AH2, P + g.aW3, g.A, g.A, nullptr, SB_NONE, o), false, true, red);
   for (int idx = tid; idx < 4 * g.A; idx += SB_NT) {
     const int a = idx >> 2, r = idx & 3;

@@ -14,6 +14,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_GEMM=f32     every GEMM on the fp32-input MFMA kernel (no twins)
     DDPG_GEMM_H=0     no twins; large GEMMs on gemm_s3 (operands split while staging)
     DDPG_THINK=0      the K <= 64 layers on the tiled GEMMs instead of thin_k
+    DDPG_SKINNY=0     the <= 64-wide weight gradients on the GEMMs instead of
+                      the skinny VALU kernel
 """
 import random
 
@@ -26,7 +28,7 @@ from test_gpu_parity import (CONFIGS, GRAD_TOL, FWD_TOL, _fill, _params, _sessio
 pytestmark = pytest.mark.gpu
 
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
-            "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL")
+            "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY")
 
 
 @pytest.fixture(scope="module")
@@ -137,6 +139,7 @@ def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
     ("DDPG_GEMM", "f32", "gemm_f32_kernel", "gemm_h"),
     ("DDPG_GEMM_H", "0", "gemm_s3_kernel", "gemm_h"),
     ("DDPG_THINK", "0", "gemm_h_kernel", "thin_k_kernel"),
+    ("DDPG_SKINNY", "0", "gemm_f32_kernel", "skinny_wgrad_kernel"),
 ])
 def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent):
     """A switch that selects different kernels: 3 fused steps at the 1024-wide
@@ -154,6 +157,20 @@ def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent)
     for (net, keys), vals in zip(nets, got["state"][:4]):
         for k, v in zip(keys, vals):
             assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (switch, net, k))
+
+
+def test_default_path_uses_skinny_wgrad(dd, O, monkeypatch):
+    """The <= 64-wide weight gradients (dW1, dWs, dWa, dW3 at S = 64, A = 16)
+    run on skinny_wgrad_kernel by default, and the 3-step oracle bars hold."""
+    _clear(monkeypatch)
+    p, _ = _params(O, "wide")
+    got = _run(dd, O, "wide", p, 3, profile=True)
+    assert "skinny_wgrad_kernel|wgrad" in got["keys"], got["keys"]
+    L, L32 = _oracle(O, "wide", p, got["rows"], 3)
+    for (net, keys), vals in zip((("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS)),
+                                 got["state"][:2]):
+        for k, v in zip(keys, vals):
+            assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (net, k))
 
 
 def test_single_rank_communicator_matches_no_communicator(dd, O, monkeypatch):
