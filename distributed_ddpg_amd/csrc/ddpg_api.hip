@@ -224,7 +224,8 @@ struct ddpg_ctx {
   bool sb_shadow_ok = false;  // cleared by every theta write outside the small path
   size_t sb_smem = 0;         // dynamic LDS bytes of the phase kernels
   float* h_pred = nullptr;    // pinned [Bmax][A]: action-selection output (written by the GPU)
-  int sb_xstride = 1;         // XCD packing of the phase kernels (env DDPG_SB_XCD=1: on)
+  int sb_xstride = 0;  // XCD packing of the phase kernels: 0 auto (on up to 32 workgroups),
+                       // env DDPG_SB_XCD=1 always (8), =0 never (1)
   unsigned long long* sb_stamps = nullptr;  // diagnostic (env DDPG_SB_STAMPS=1)
 
   // kernel-path switches, read from the environment at ddpg_create (each is
@@ -1443,7 +1444,9 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   a.cWo = L.c[CWO].off;
   a.cbo = L.c[CBO].off;
   a.stamps = c->sb_stamps;
-  a.xstride = c->sb_xstride;
+  // all workgroups on one XCD (one L2 streams the weights) while they fit its
+  // 32 CUs: +3 % at C2 (profiles/r3/sb_xcd_ab_c2.txt)
+  a.xstride = c->sb_xstride ? c->sb_xstride : (ceil_div(B, SB_R) <= 32 ? 8 : 1);
   return a;
 }
 

@@ -7,7 +7,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_XCD=0        no XCD-aware tile order
     DDPG_XCD_RECT=0   row-major XCD runs instead of per-XCD tile rectangles
     DDPG_PAR=1        independent branches forked onto two aux streams
-    DDPG_SB_XCD=1     small-batch workgroups packed on one XCD
+    DDPG_SB_XCD=0     small-batch workgroups dealt over the XCDs (the default
+                      packs up to 32 of them on one XCD)
     DDPG_GEMM_MF=32   bf16 config on the 32x32x16 twin GEMM (same per-output
                       summation order as the default 16x16x32 kernel)
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
@@ -109,7 +110,7 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_XCD", "0", "wide"),
     ("DDPG_XCD_RECT", "0", "wide"),
     ("DDPG_PAR", "1", "wide"),
-    ("DDPG_SB_XCD", "1", "ip"),
+    ("DDPG_SB_XCD", "0", "ip"),
 ])
 def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
