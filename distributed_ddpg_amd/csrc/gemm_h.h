@@ -51,18 +51,19 @@ struct GemmHArgs {
 
 constexpr int HG_NT = 512, HG_BN = 128, HG_STAGES = 3;
 
-template <int BM, int BK, int NP>
+template <int BM, int BK, int NP, int NW = 8>
 struct HgCfg {
   static constexpr int A_BYTES = BM * BK * 2;  // one plane, one stage
   static constexpr int B_BYTES = HG_BN * BK * 2;
   static constexpr int STAGE = NP * (A_BYTES + B_BYTES);
-  static constexpr int A_PW = A_BYTES / 1024 / 8;  // 1-KiB pieces per wave per plane
-  static constexpr int B_PW = B_BYTES / 1024 / 8;
+  static constexpr int A_PW = A_BYTES / 1024 / NW;  // 1-KiB pieces per wave per plane
+  static constexpr int B_PW = B_BYTES / 1024 / NW;
   static constexpr int G = NP * (A_PW + B_PW);  // glds instructions per wave per k-tile
   static constexpr int EPI_BYTES = TileCfg<BM, HG_BN>::EPI * 4;
   static constexpr int SMEM_BYTES =
       HG_STAGES * STAGE > EPI_BYTES ? HG_STAGES * STAGE : EPI_BYTES;
-  static_assert(A_PW >= 1 && B_PW >= 1 && A_PW * 8192 == A_BYTES && B_PW * 8192 == B_BYTES,
+  static_assert(A_PW >= 1 && B_PW >= 1 && A_PW * 1024 * NW == A_BYTES &&
+                    B_PW * 1024 * NW == B_BYTES,
                 "tile must split into whole 1-KiB pieces per wave");
   static_assert(SMEM_BYTES <= 160 * 1024, "LDS");
 };
@@ -217,10 +218,19 @@ DDPG_DEV void hg_wait16(bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
 // step ks (two read groups per MFMA gap, in program order pinned by
 // sched_barriers) instead of issued as one burst ahead of them, and the
 // tile-(t+2) glds sit in the MFMA gaps after the reads.
-template <int AL, int BL, int NP, int BM, int BK, int SCH = 0>
-__global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
-  using C = HgCfg<BM, BK, NP>;
+//
+// WGN: waves along N.  4 (default): 8 waves, wave tile (BM/2) x 32.  2: 4
+// waves (one per SIMD), wave tile (BM/2) x 64 -- every A fragment feeds two
+// B fragments: a k-step reads NP (TM + TN) fragments for 6 TM TN MFMAs (NP =
+// 3, BM = 128: 12 reads per 24 MFMAs instead of 9 per 12, so 2/3 of the LDS
+// read bytes per MFMA).
+template <int AL, int BL, int NP, int BM, int BK, int SCH = 0, int WGN = 4>
+__global__ __launch_bounds__(128 * WGN, 1) void gemm_h_kernel(GemmHArgs g) {
+  constexpr int NW = 2 * WGN, NT = 64 * NW;
+  using C = HgCfg<BM, BK, NP, NW>;
   constexpr int TM = BM / 64;
+  constexpr int TN = 4 / WGN;      // 32-column MFMA tiles per wave
+  constexpr int WCOL = HG_BN / WGN;  // columns per wave
   constexpr int KS = BK / 16;
   static_assert(KS % 2 == 0, "fragment register sets alternate by k-step parity");
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM_BYTES / 4];
@@ -228,7 +238,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WGN, wn = wave % WGN;
   int bx, by;
   xcd_tile(bx, by, g.xcd);
   const int n0 = bx * HG_BN, m0 = by * BM, z = blockIdx.z;
@@ -236,19 +246,23 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   const int kend = min(g.K, kbeg + g.kps);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
 
-  f32x16 acc[TM][1];
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   // NP = 3: the five small plane products go to their own accumulators, so
   // the main (hh) chain takes one rounding per k-step instead of six
-  f32x16 acs[NP == 3 ? TM : 1];
+  f32x16 acs[NP == 3 ? TM : 1][NP == 3 ? TN : 1];
   if constexpr (NP == 3) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acs[i][r] = 0.f;
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acs[i][j][r] = 0.f;
   }
 
   const __bf16* sa[C::A_PW];
@@ -282,52 +296,62 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
     for (int q = 0; q < C::G; ++q) piece(t, buf, q);
   };
 
-  auto read = [&](const char* base, int ks, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+  auto read = [&](const char* base, int ks, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP][TN]) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      bv[p] = hg_frag<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[p][j] = hg_frag<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * WCOL + 32 * j,
+                                   ks, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
         av[p][i] = hg_frag<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 32 * i, ks, lane);
     }
   };
-  auto mfma_i = [&](int i, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
-    if constexpr (NP == 3) {
-      // small terms, smallest first: lh, mm, hl, mh, hm  (planes 0 = h, 1 = m, 2 = l)
-      f32x16 c = acs[i];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], c, 0, 0, 0);
-      acs[i] = c;
+  auto mfma_i = [&](int i, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP][TN]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (NP == 3) {
+        // small terms, smallest first: lh, mm, hl, mh, hm  (planes 0 = h, 1 = m, 2 = l)
+        f32x16 c = acs[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], c, 0, 0, 0);
+        acs[i][j] = c;
+      }
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
     }
-    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
   };
 
-  // read group j (0 .. NP * (TM + 1) - 1) of step ks: plane j / (TM + 1),
-  // fragment j % (TM + 1) (0: the B fragment, 1 ..: A fragment i - 1)
-  auto read_one = [&](const char* base, int ks, int j, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
-    const int p = j / (TM + 1), f = j % (TM + 1);
-    if (f == 0)
-      bv[p] = hg_frag<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * 32, ks, lane);
+  // read group j (0 .. NP * (TM + TN) - 1) of step ks: plane j / (TM + TN),
+  // fragment f = j % (TM + TN) (f < TN: B fragment f, then A fragment f - TN)
+  auto read_one = [&](const char* base, int ks, int j, bf16x8 (&av)[NP][TM],
+                      bf16x8 (&bv)[NP][TN]) {
+    const int p = j / (TM + TN), f = j % (TM + TN);
+    if (f < TN)
+      bv[p][f] = hg_frag<BL, BK>(base + NP * C::A_BYTES + p * C::B_BYTES, wn * WCOL + 32 * f, ks,
+                                 lane);
     else
-      av[p][f - 1] = hg_frag<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 32 * (f - 1), ks, lane);
+      av[p][f - TN] =
+          hg_frag<AL, BK>(base + p * C::A_BYTES, wm * (BM / 2) + 32 * (f - TN), ks, lane);
   };
-  // the 6 (NP = 3) or 1 MFMAs of output block i as a flat list, MFMA q of block i
-  auto mfma_q = [&](int i, int q, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP]) {
+  // the 6 (NP = 3) or 1 MFMAs of output block b = (i, j) as a flat list
+  auto mfma_q = [&](int b, int q, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP][TN]) {
+    const int i = b / TN, j = b % TN;
     if constexpr (NP == 3) {
-      if (q == 0) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0], acs[i], 0, 0, 0);
-      if (q == 1) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1], acs[i], 0, 0, 0);
-      if (q == 2) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2], acs[i], 0, 0, 0);
-      if (q == 3) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0], acs[i], 0, 0, 0);
-      if (q == 4) acs[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1], acs[i], 0, 0, 0);
+      if (q == 0) acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], acs[i][j], 0, 0, 0);
+      if (q == 1) acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], acs[i][j], 0, 0, 0);
+      if (q == 2) acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], acs[i][j], 0, 0, 0);
+      if (q == 3) acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], acs[i][j], 0, 0, 0);
+      if (q == 4) acs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], acs[i][j], 0, 0, 0);
     }
     if (q == (NP == 3 ? 5 : 0))
-      acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0], acc[i][0], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
   };
 
-  bf16x8 fa[2][NP][TM], fb[2][NP];
+  bf16x8 fa[2][NP][TM], fb[2][NP][TN];
   // glds of the next-but-one tile are spread over the first KS-1 k-steps
   constexpr int GSEG = KS - 1;
   // one k-tile; STAGE_NEXT2: stage tile t+2; HAS_NEXT: tile t+1 exists
@@ -340,7 +364,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
       constexpr int ks = decltype(ks_c)::value;
       auto& av = fa[ks & 1];
       auto& bv = fb[ks & 1];
-      hg_wait<0, NP, TM>(av, bv);
+      hg_wait16<NP, TM, TN>(av, bv);
       if constexpr (ks + 1 < KS) {
         read(base, ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
       } else if constexpr (HAS_NEXT) {
@@ -360,7 +384,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
 #pragma unroll
         for (int q = lo; q < hi; ++q) piece(t + 2, sbuf, q);
         // MFMAs and glds alternate (MPG MFMAs, one glds, ...)
-        constexpr int NM = TM * (NP == 3 ? 6 : 1), NG = hi - lo;
+        constexpr int NM = TM * TN * (NP == 3 ? 6 : 1), NG = hi - lo;
         constexpr int MPG = NG > 0 ? NM / NG : NM;
         static_for<NG>([&](auto) {
           __builtin_amdgcn_sched_group_barrier(0x008, MPG, 0);
@@ -375,8 +399,8 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
 
   // SCH = 1 k-tile: per k-step, wait own reads | (last step: vmcnt, barrier) |
   // MFMA q, then read groups / glds in its gap, in pinned program order
-  constexpr int NRG = NP * (TM + 1);       // read groups per k-step
-  constexpr int NMF = TM * (NP == 3 ? 6 : 1);  // MFMAs per k-step
+  constexpr int NRG = NP * (TM + TN);       // read groups per k-step
+  constexpr int NMF = TM * TN * (NP == 3 ? 6 : 1);  // MFMAs per k-step
   auto tile_il = [&](int t, auto stage_c, auto next_c) {
     constexpr bool STAGE_NEXT2 = decltype(stage_c)::value;
     constexpr bool HAS_NEXT = decltype(next_c)::value;
@@ -391,7 +415,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
       constexpr int rks = ks + 1 < KS ? ks + 1 : 0;
       auto& nav = fa[(ks + 1) & 1];
       auto& nbv = fb[(ks + 1) & 1];
-      hg_wait<0, NP, TM>(av, bv);
+      hg_wait16<NP, TM, TN>(av, bv);
       if constexpr (ks + 1 == KS && HAS_NEXT) {
         if constexpr (STAGE_NEXT2)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
@@ -450,7 +474,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   }
   if constexpr (NP == 3) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] += acs[i];
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += acs[i][j];
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // staging buffers are reused by the epilogue
@@ -458,7 +484,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h_kernel(GemmHArgs g) {
   ge.M = g.M;
   ge.N = g.N;
   ge.e = g.e;
-  gemm_epilogue<BM, HG_BN, 4>(acc, smem, ge, tid, n0, m0, z, bx, by);
+  gemm_epilogue<BM, HG_BN, WGN>(acc, smem, ge, tid, n0, m0, z, bx, by);
 }
 
 // The same GEMM on v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md "DVFS

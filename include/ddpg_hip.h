@@ -31,6 +31,10 @@
 extern "C" {
 #endif
 
+/* ABI 2 (behaviour change from 1): the 1:1 methods no longer apply the scaler
+ * set by ddpg_set_scaler -- callers pass preprocessed states (see there); only
+ * the fused step's replay gathers scale.  Pinned by
+ * tests/test_gpu_configs.py::test_mountaincar_scaler_parity (1:1 and fused). */
 #define DDPG_ABI_VERSION 2
 
 enum ddpg_status {

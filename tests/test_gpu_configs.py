@@ -234,6 +234,9 @@ def test_data_parallel_rank_slices_sum_to_global(dd, O, monkeypatch):
 
 # ---------------------------------------------------------------- C5
 BF16_FWD_TOL, BF16_DA_TOL, BF16_GRAD_NORM_TOL, BF16_PARAM_TOL = 2e-2, 5e-2, 3e-2, 2e-2
+# Adam first-moment slot after the first step, m = (1 - beta1) g: max-rel bar
+# (max |m - 0.1 g_ref| / max |0.1 g_ref|) against the float64 oracle gradient
+BF16_M_MAXREL = 5e-2
 
 
 def test_c5_bf16_full_dims(dd, O):
@@ -275,15 +278,44 @@ def test_c5_bf16_full_dims(dd, O):
                            (_lib.ACTOR_GRAD, out["actor_grads"], O.ACTOR_KEYS)):
         for k, g in zip(keys_, sess.get_params(gw)):
             assert normrel(g, ref[k]) < BF16_GRAD_NORM_TOL, ("grad", k, normrel(g, ref[k]))
-    # parameters after the step: TF Adam's first step moves every element by
-    # ~lr * sign(g), so a bf16 gradient whose sign flips near zero costs at most
-    # two steps; bound every element by 2 lr (plus fp32 rounding) and the weight
-    # matrices by the max-rel bar as well
-    for which, net, names, lr in ((_lib.ACTOR, "actor", O.ACTOR_KEYS, 1e-4),
-                                  (_lib.CRITIC, "critic", O.CRITIC_KEYS, 1e-3)):
+    # Adam slots after the first step (fresh state): m = (1 - beta1) g and
+    # v = (1 - beta2) g^2 of the GPU's own gradient, and m against the
+    # oracle's gradient at the stated bf16 max-rel bar
+    for gw, mw, vw, ref, keys_ in (
+            (_lib.CRITIC_GRAD, _lib.CRITIC_ADAM_M, _lib.CRITIC_ADAM_V, out["critic_grads"],
+             O.CRITIC_KEYS),
+            (_lib.ACTOR_GRAD, _lib.ACTOR_ADAM_M, _lib.ACTOR_ADAM_V, out["actor_grads"],
+             O.ACTOR_KEYS)):
+        for k, g, m, v in zip(keys_, sess.get_params(gw), sess.get_params(mw), sess.get_params(vw)):
+            g64, r = np.asarray(g, np.float64), 0.1 * np.asarray(ref[k], np.float64).reshape(g.shape)
+            # TF ApplyAdam takes 1 - beta in fp32: 0.100000024, 0.00099998713
+            c1 = float(np.float32(1) - np.float32(0.9))
+            c2 = float(np.float32(1) - np.float32(0.999))
+            assert np.max(np.abs(m - c1 * g64)) <= 1e-6 * np.max(np.abs(c1 * g64)) + 1e-30, ("m", k)
+            assert np.max(np.abs(v - c2 * g64 * g64)) <= 1e-6 * np.max(c2 * g64 * g64) + 1e-30, \
+                ("v", k)
+            mr = np.max(np.abs(m - r)) / max(np.max(np.abs(r)), 1e-30)
+            assert mr < BF16_M_MAXREL, ("m vs oracle", k, mr)
+    # parameters after the step.  TF Adam's first step moves an element by
+    # lr * g / (|g| + eps / sqrt(1 - beta2)) = lr * sign(g) for |g| >> 3e-7:
+    # where the oracle's gradient is at least a tenth of its maximum (no bf16
+    # sign flip possible there) the step must be -lr * sign(g_ref) to 1 % of lr;
+    # elsewhere a sign flipped near zero costs at most two steps (2 lr), and the
+    # weight matrices also meet the max-rel bar
+    for which, net, names, lr, grads in ((_lib.ACTOR, "actor", O.ACTOR_KEYS, 1e-4,
+                                          out["actor_grads"]),
+                                         (_lib.CRITIC, "critic", O.CRITIC_KEYS, 1e-3,
+                                          out["critic_grads"])):
         for k, v in zip(names, sess.get_params(which)):
             r = L.state()[net][k].reshape(v.shape)
             assert np.max(np.abs(v - r)) <= 2.02 * lr, (net, k, np.max(np.abs(v - r)))
             if k.startswith("W") and v.size >= 64 * 64:
                 assert rel(v, r) < BF16_PARAM_TOL, (net, k)
+            g = np.asarray(grads[k], np.float64).reshape(v.shape)
+            big = np.abs(g) >= 0.1 * np.max(np.abs(g))
+            th0 = np.asarray(p[net][k], np.float64).reshape(v.shape)
+            step = np.asarray(v, np.float64) - th0
+            tol = 0.01 * lr + 4 * np.spacing(np.abs(th0).astype(np.float32)).astype(np.float64)
+            bad = big & (np.abs(step + lr * np.sign(g)) > tol)
+            assert not bad.any(), (net, k, int(bad.sum()), int(big.sum()))
     sess.close()

@@ -73,7 +73,7 @@ struct Case {
 static float *gA, *gB, *gC, *gR, *gBias;
 static __bf16 *hA, *hB, *gTw;
 
-template <int AL, int BL, int NP, int BM, int BK, int MF, int SCH = 0>
+template <int AL, int BL, int NP, int BM, int BK, int MF, int SCH = 0, int WGN = 4>
 static void run_case(const Case& c) {
   const size_t na = (size_t)c.M * c.K, nb = (size_t)c.K * c.N, nc = (size_t)c.M * c.N;
   // fresh operands (NP = 1 rounds them), planes
@@ -137,12 +137,12 @@ static void run_case(const Case& c) {
     if constexpr (MF == 16)
       hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, NP, BM, BK, SCH>), grid, dim3(HG_NT), 0, 0, g);
     else
-      hipLaunchKernelGGL((gemm_h_kernel<AL, BL, NP, BM, BK, SCH>), grid, dim3(HG_NT), 0, 0, g);
+      hipLaunchKernelGGL((gemm_h_kernel<AL, BL, NP, BM, BK, SCH, WGN>), grid, dim3(128 * WGN), 0, 0, g);
   };
   const float us = time_it(f, 10);
   if (epi) {  // elu'd outputs: timing only
-    printf("%-26s MF%d S%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d EPI%d  %8.2f us %7.1f TF\n", c.name,
-           MF, SCH, NP, BM, BK, c.M, c.N, c.K, c.splits, epi, us,
+    printf("%-26s MF%d S%d W%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d EPI%d  %8.2f us %7.1f TF\n", c.name,
+           MF, SCH, WGN, NP, BM, BK, c.M, c.N, c.K, c.splits, epi, us,
            2.0 * c.M * c.N * (double)c.K / (us * 1e-6) / 1e12);
     fflush(stdout);
     return;
@@ -181,18 +181,18 @@ static void run_case(const Case& c) {
   const double flop = 2.0 * c.M * c.N * (double)c.K;
   const double tf = flop / (us * 1e-6) / 1e12;
   const double peak = NP == 3 ? 2500.0 / 6 : 2500.0;
-  printf("%-26s MF%d S%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d  %8.2f us %7.1f TF (%5.1f%% of %.0f)  "
+  printf("%-26s MF%d S%d W%d NP=%d BM=%d BK=%d M=%d N=%d K=%d s=%d  %8.2f us %7.1f TF (%5.1f%% of %.0f)  "
          "vs f32 %.2e | vs f64: gemm_h %.2e, f32 MFMA %.2e | out %.9e\n",
-         c.name, MF, SCH, NP, BM, BK, c.M, c.N, c.K, c.splits, us, tf, 100.0 * tf / peak, peak,
+         c.name, MF, SCH, WGN, NP, BM, BK, c.M, c.N, c.K, c.splits, us, tf, 100.0 * tf / peak, peak,
          maxerr / maxref, e64h / m64, e64r / m64, (double)out[nc / 3 + 7]);
   fflush(stdout);
 }
 
-template <int NP, int BM, int BK, int MF, int SCH = 0>
+template <int NP, int BM, int BK, int MF, int SCH = 0, int WGN = 4>
 static void dispatch1(const Case& c) {
-  if (c.al == L_RK && c.bl == L_KR) run_case<L_RK, L_KR, NP, BM, BK, MF, SCH>(c);
-  if (c.al == L_RK && c.bl == L_RK) run_case<L_RK, L_RK, NP, BM, BK, MF, SCH>(c);
-  if (c.al == L_KR && c.bl == L_KR) run_case<L_KR, L_KR, NP, BM, BK, MF, SCH>(c);
+  if (c.al == L_RK && c.bl == L_KR) run_case<L_RK, L_KR, NP, BM, BK, MF, SCH, WGN>(c);
+  if (c.al == L_RK && c.bl == L_RK) run_case<L_RK, L_RK, NP, BM, BK, MF, SCH, WGN>(c);
+  if (c.al == L_KR && c.bl == L_KR) run_case<L_KR, L_KR, NP, BM, BK, MF, SCH, WGN>(c);
 }
 // the 32x32x16 kernel (both schedules) and the 16x16x32 kernel on the same
 // case, interleaved
@@ -201,6 +201,11 @@ static void dispatch(const Case& c) {
   for (int rep = 0; rep < 2; ++rep) {
     dispatch1<NP, BM, BK, 32, 0>(c);
     dispatch1<NP, BM, BK, 32, 1>(c);
+    // env GH_W2=1: also the 4-wave form (WGN = 2, wave tile BM/2 x 64)
+    if (getenv("GH_W2") && atoi(getenv("GH_W2"))) {
+      dispatch1<NP, BM, BK, 32, 0, 2>(c);
+      dispatch1<NP, BM, BK, 32, 1, 2>(c);
+    }
     if constexpr (NP == 1) {
       dispatch1<NP, BM, BK, 16, 0>(c);
       dispatch1<NP, BM, BK, 16, 1>(c);
