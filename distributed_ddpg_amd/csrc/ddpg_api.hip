@@ -238,6 +238,7 @@ struct ddpg_ctx {
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
+    bool l1_batch = true;  // DDPG_L1BATCH=0: the step's first layers per network
   } sw;
 
   // comm: every collective of the ctx is issued on cs (one stream, so the
@@ -679,12 +680,12 @@ static TkPart tk_part(const float* X, int ldx, int K, const float* W, int ldw, i
   return p;
 }
 
-// Launch 1 or 2 thin-K parts over M rows; returns the number of 64-row blocks
-// (the row count of colsum partials), or 0 (nothing launched) when the layer
-// is not eligible and the caller must use the GEMM.
+// Launch 1 .. TK_MAXP thin-K parts over M rows; returns the number of 64-row
+// blocks (the row count of colsum partials), or 0 (nothing launched) when a
+// layer is not eligible and the caller must use the GEMM.
 static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M) {
-  if (!c->sw.thin_k) return 0;
-  TkPart pp[2];
+  if (!c->sw.thin_k || nparts < 1 || nparts > TK_MAXP) return 0;
+  TkPart pp[TK_MAXP];
   for (int i = 0; i < nparts; ++i) {
     pp[i] = parts[i];
     // K-padded to the 8-step of the kernel over zero-padded rows (the W rows
@@ -726,14 +727,11 @@ static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int
 // ====================================================================== building blocks
 static const float* P(ddpg_ctx* c, const float* base, const Tensor& t) { return base + t.off; }
 
-// Actor forward (networks.py:51-63) on [B][ldS] states.
-// h1 is always materialised (input of layer 2); h2 only when h2 != nullptr.
-static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, float* h1,
-                      float* h2, float* o, float* mu) {
+// The actor's first layer as a thin-K part.  The target path's h1 is read only
+// by the next layer: when that runs on the twin GEMM, only the twin is written.
+static TkPart actor_l1_part(ddpg_ctx* c, const float* base, const float* s, int B, float* h1,
+                            Twin* twin) {
   const Layout& L = c->L;
-  GemmEpi e = epi_none();
-  // the target path's h1 is read only by the next layer: when that runs on
-  // the twin GEMM, only the twin is written
   int kh;
   const Twin h1t = (h1 == c->th1 && gemm_h_ok<L_RK, L_KR>(c, h1, c->ldAH1, P(c, base, L.a[AW2]),
                                                            c->AH2, B, c->AH2, c->AH1, 1, &kh))
@@ -744,7 +742,20 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
   tp.outh = h1t.p;
   tp.hps = h1t.ps;
   tp.hnp = c->hnp;
-  if (!thin_k_launch(c, "fwd", &tp, 1, B)) {
+  if (twin) *twin = h1t;
+  return tp;
+}
+
+// Actor forward (networks.py:51-63) on [B][ldS] states.
+// h1 is always materialised (input of layer 2); h2 only when h2 != nullptr.
+// l1_done: h1 was already produced (first_layers_dev).
+static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, float* h1,
+                      float* h2, float* o, float* mu, bool l1_done = false) {
+  const Layout& L = c->L;
+  GemmEpi e = epi_none();
+  Twin h1t;
+  const TkPart tp = actor_l1_part(c, base, s, B, h1, &h1t);
+  if (!l1_done && !thin_k_launch(c, "fwd", &tp, 1, B)) {
     e.out = h1t.p ? nullptr : h1;
     e.outh = h1t.p;
     e.h_plane_stride = h1t.ps;
@@ -778,29 +789,52 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
 //   1: proj(Wo) -> qpart only (predict / target)
 //   2: dh_pre = Wo[j] * elu'(h) -> dhp_out (action-gradient path, grad_ys = 1)
 // Returns the number of qpart slabs (modes 0/1).
-static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const float* a, int B,
-                      float* cat, float* h_out, int mode, float* dhp_out) {
+// The critic's first layer, [state branch | action branch] of the concat, as
+// two thin-K parts.  The target path's concat is read only by the hidden
+// layer: when that runs on the twin GEMM, only the twin is written.
+static Twin critic_l1_parts(ddpg_ctx* c, const float* base, const float* s, const float* a, int B,
+                            float* cat, TkPart tp[2]) {
   const Layout& L = c->L;
-  GemmEpi e = epi_none();
-  // the target path's concat is read only by the hidden layer: when that runs
-  // on the twin GEMM, only the twin is written
   int kh;
   const Twin ct = (cat == c->tcat && gemm_h_ok<L_RK, L_KR>(c, cat, c->ldC, P(c, base, L.c[CWH]),
                                                             c->CH2, B, c->CH2, 2 * c->CH1, 1, &kh))
                       ? act_twin(c, cat)
                       : Twin();
-  // [state branch | action branch] of the concat in one launch
-  TkPart tp[2] = {tk_part(s, c->ldS, c->S, P(c, base, L.c[CWS]), c->CH1, 0, c->CH1,
-                          P(c, base, L.c[CBS]), 1, ct.p ? nullptr : cat, c->ldC),
-                  tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1,
-                          P(c, base, L.c[CBA]), 1, ct.p ? nullptr : cat + c->CH1, c->ldC)};
+  tp[0] = tk_part(s, c->ldS, c->S, P(c, base, L.c[CWS]), c->CH1, 0, c->CH1, P(c, base, L.c[CBS]),
+                  1, ct.p ? nullptr : cat, c->ldC);
+  tp[1] = tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1, P(c, base, L.c[CBA]),
+                  1, ct.p ? nullptr : cat + c->CH1, c->ldC);
   if (ct.p)
     for (int i = 0; i < 2; ++i) {
       tp[i].outh = ct.p + i * c->CH1;
       tp[i].hps = ct.ps;
       tp[i].hnp = c->hnp;
     }
-  if (!thin_k_launch(c, "fwd", tp, 2, B)) {  // each branch on its own
+  return ct;
+}
+
+// l1_done: 0 compute both first-layer branches, 1 the state branch is
+// already in `cat` (first_layers_dev), 2 both are.
+static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const float* a, int B,
+                      float* cat, float* h_out, int mode, float* dhp_out, int l1_done = 0) {
+  const Layout& L = c->L;
+  GemmEpi e = epi_none();
+  int kh;
+  TkPart tp[2];
+  const Twin ct = critic_l1_parts(c, base, s, a, B, cat, tp);
+  if (l1_done == 1) {
+    if (!thin_k_launch(c, "fwd", &tp[1], 1, B)) {
+      e.ldo = c->ldC;
+      e.act = 1;
+      e.h_plane_stride = ct.ps;
+      e.h_planes = c->hnp;
+      e.out = ct.p ? nullptr : cat + c->CH1;
+      e.outh = ct.p ? ct.p + c->CH1 : nullptr;
+      e.bias = P(c, base, L.c[CBA]);
+      gemm_launch<L_RK, L_KR>(c, "fwd", a, c->ldA, P(c, base, L.c[CWA]), c->CH1, B, c->CH1,
+                              c->A, e);
+    }
+  } else if (l1_done == 0 && !thin_k_launch(c, "fwd", tp, 2, B)) {  // each branch on its own
     e.ldo = c->ldC;
     e.act = 1;
     e.h_plane_stride = ct.ps;
@@ -1325,18 +1359,41 @@ static void soft_update_dev(ddpg_ctx* c, int mask, int pw_mask) {
 // (aux[0]), the online actor forward (aux[1]) and the online critic forward
 // (main) are independent until the critic loss; inside the backward passes
 // the weight-gradient GEMMs run beside the dX chain.
+// The five first layers of a large-batch step that depend only on the batch
+// and the pre-step parameters (target actor on s2, the target critic's state
+// branch on s2, actor on s, the critic's state and action branches on (s, a))
+// as ONE thin-K launch: one ramp and tail instead of four, 5 x 512 blocks to
+// fill the chip.  Returns false (nothing launched) when a part is not
+// thin-K-eligible; the per-network paths then compute them as before.
+static bool first_layers_dev(ddpg_ctx* c, int B) {
+  if (!c->sw.thin_k || !c->sw.l1_batch) return false;
+  TkPart tp[TK_MAXP], tc[2];
+  tp[0] = actor_l1_part(c, c->target, c->s2, B, c->th1, nullptr);
+  critic_l1_parts(c, c->target, c->s2, c->ta2, B, c->tcat, tc);
+  tp[1] = tc[0];
+  tp[2] = actor_l1_part(c, c->theta, c->s, B, c->h1, nullptr);
+  critic_l1_parts(c, c->theta, c->s, c->a, B, c->cat, tc);
+  tp[3] = tc[0];
+  tp[4] = tc[1];
+  return thin_k_launch(c, "fwd_l1", tp, TK_MAXP, B) != 0;
+}
+
 static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   const Layout& L = c->L;
   const hipStream_t s0 = c->cur;
   const hipStream_t s1 = c->par ? c->aux[0] : s0, s2 = c->par ? c->aux[1] : s0;
+  // ddpg.py:90-109's batch-only first layers, all at once (every later use
+  // reads them with the same pre-step parameters)
+  const bool l1 = first_layers_dev(c, B);
   fork_to(c, 0, s0, s1);
   fork_to(c, 0, s0, s2);
   // target_q = critic.predict_target(s2, actor.predict_target(s2))  ddpg.py:90
   c->cur = s1;
   std::swap(c->ppart, c->ppart_t);
   std::swap(c->qpart, c->qpart_t);
-  actor_fwd(c, c->target, c->s2, B, c->th1, nullptr, nullptr, c->ta2);
-  const int nqt = critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr);
+  actor_fwd(c, c->target, c->s2, B, c->th1, nullptr, nullptr, c->ta2, l1);
+  const int nqt =
+      critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr, l1 ? 1 : 0);
   {
     ProfScope ps(c, "td_target", 0, 0);
     hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->cur, c->qpart,
@@ -1348,10 +1405,10 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   std::swap(c->qpart, c->qpart_t);
   // a_outs = actor.predict(s)  ddpg.py:106 (actor params are unchanged until actor.train)
   c->cur = s2;
-  actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu);
+  actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu, l1);
   // critic.train(s, a, y)  ddpg.py:100: forward now, loss once y is ready
   c->cur = s0;
-  const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
+  const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr, l1 ? 2 : 0);
   fork_to(c, 1, s1, s0);  // join target path (y)
   critic_train_dev(c, B, inv_b, true, nq, c->par);
   // grads = critic.action_gradients(s, a_outs)  ddpg.py:107 (updated critic)
@@ -1685,6 +1742,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
+      c->sw.l1_batch = !env_is("DDPG_L1BATCH", "0");
     }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;

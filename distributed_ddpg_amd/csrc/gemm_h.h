@@ -226,7 +226,7 @@ DDPG_DEV void hg_wait16(bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
 // read bytes per MFMA).
 template <int AL, int BL, int NP, int BM, int BK, int SCH = 0, int WGN = 4>
 __global__ __launch_bounds__(128 * WGN, 1) void gemm_h_kernel(GemmHArgs g) {
-  constexpr int NW = 2 * WGN, NT = 64 * NW;
+  constexpr int NW = 2 * WGN;
   using C = HgCfg<BM, BK, NP, NW>;
   constexpr int TM = BM / 64;
   constexpr int TN = 4 / WGN;      // 32-column MFMA tiles per wave

@@ -13,9 +13,11 @@
 // (gemm_h.h) per 16-deep step on v_mfma_f32_32x32x16_bf16 with fp32
 // accumulation -- 2.7x the fp32-input MFMA rate at the same accuracy class as
 // the large GEMMs.  The fused epilogue has the gemm_common.h semantics (bias,
-// elu, EluGrad multiply, bias-gradient column sums).  Two independent layers
-// writing different column ranges of one output (the critic's [state |
-// action] concat) share one launch (blockIdx.z selects the part).
+// elu, EluGrad multiply, bias-gradient column sums).  Up to TK_MAXP
+// independent layers share one launch (blockIdx.z selects the part): the
+// critic's [state | action] concat, and the large-batch step's five
+// batch-only first layers (target actor, target critic state branch, actor,
+// critic state and action branches).
 #pragma once
 #include "common.h"
 
@@ -58,8 +60,10 @@ struct TkPart {
   int ld_colsum;
 };
 
+constexpr int TK_MAXP = 5;  // parts per launch (blockIdx.z)
+
 struct TkArgs {
-  TkPart p[2];
+  TkPart p[TK_MAXP];
   int M;
 };
 
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   char* const ximg = lds + TK_WREG;
   // column-sum scratch: the X image, dead after the MFMA phase
   float* const red = reinterpret_cast<float*>(ximg);
-  const TkPart P = blockIdx.z ? args.p[1] : args.p[0];
+  const TkPart P = args.p[blockIdx.z];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, h = lane >> 5;
   const int wr = wave & 1, wc = wave >> 1;  // 32-row half, column half
