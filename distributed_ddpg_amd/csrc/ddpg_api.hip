@@ -1018,17 +1018,22 @@ static void cs_link(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
 // In-place RCCL sums of up to 2 disjoint ranges of the flat grad buffer, on
 // the comm stream after the work queued so far on c->cur (one group: one
 // launch).  The caller joins cs back before the gradients are read.
+// with_stats: the all-gather of the step's {q_max, loss} joins the same group
+// (one collective launch, one latency on the critical path instead of two);
+// stats_allreduce_on_cs then only reduces the gathered values.
 static void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0,
-                            float* b1 = nullptr, size_t n1 = 0) {
+                            float* b1 = nullptr, size_t n1 = 0, bool with_stats = false) {
   if (!c->comm) return;
   cs_link(c, ev, c->cur, c->cs);
   const hipStream_t prev = c->cur;
   c->cur = c->cs;
   {
-    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0);
+    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0 + (with_stats ? 8.0 * c->world : 0.0));
     nccl_try(ncclGroupStart());
     if (n0) nccl_try(ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs));
     if (n1) nccl_try(ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs));
+    if (with_stats)
+      nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
     nccl_try(ncclGroupEnd());
   }
   c->cur = prev;
@@ -1040,13 +1045,14 @@ static void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, si
 // all-gather of every rank's {q_max, loss}, then an ordered reduction that
 // every rank computes identically; it also feeds the running sums.  On the
 // comm stream, after the critic all-reduce.
-static void stats_allreduce_on_cs(ddpg_ctx* c) {
+static void stats_allreduce_on_cs(ddpg_ctx* c, bool gathered = false) {
   if (!c->comm) return;
   const hipStream_t prev = c->cur;
   c->cur = c->cs;
   {
-    ProfScope ps(c, "rccl_stats", 0, 8.0 * c->world);
-    nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
+    ProfScope ps(c, "rccl_stats", 0, gathered ? 0.0 : 8.0 * c->world);
+    if (!gathered)
+      nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
     hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cs, c->dstats_all, c->world,
                        c->dstats, c->dacc);
     HIP_TRY(hipGetLastError());
@@ -1205,8 +1211,8 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
     // the rest of the critic ([Ws bs Wa ba] and [bh Wo bo]) behind dWh on the
     // comm stream, then the stats; Adam waits for all of it
     allreduce_on_cs(c, 1, "rccl_allreduce", G + L.critic_begin, L.c[CWH].off - L.critic_begin,
-                    G + L.c[CBH].off, L.critic_end - L.c[CBH].off);
-    stats_allreduce_on_cs(c);
+                    G + L.c[CBH].off, L.critic_end - L.c[CBH].off, true);
+    stats_allreduce_on_cs(c, true);
     join_cs(c, 2);
   }
   adam_launch(c, 1, !fused, fused);
