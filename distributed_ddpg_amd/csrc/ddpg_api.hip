@@ -239,6 +239,7 @@ struct ddpg_ctx {
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
     bool l1_batch = true;  // DDPG_L1BATCH=0: the step's first layers per network
+    bool act_planes = true;  // DDPG_ACT32=1: fp32 copies of h1 / cat / cat2 as well
   } sw;
 
   // comm: every collective of the ctx is issued on cs (one stream, so the
@@ -393,6 +394,22 @@ static Twin act_twin(const ddpg_ctx* c, const float* q) {
       return t;
     }
   return t;
+}
+
+enum { ACT_H1, ACT_CAT, ACT_CAT2 };
+static bool gemm_h_ok_fwd_l2(ddpg_ctx* c, int which, int B);  // below
+
+// fp32 contexts: an activation whose every reader takes its three exact bf16
+// planes (the twin GEMMs, and the EluGrad factor of the next backward GEMM's
+// epilogue, `GemmEpi::auxh`) is written as planes only -- 4 B per element
+// less to write for 2 B more to read.  h1 (actor layer 1), cat (critic layer
+// 1, train / predict) and cat2 (critic layer 1 at (s, mu)).  DDPG_ACT32=1
+// keeps the fp32 copies.
+static bool act_planes_only(ddpg_ctx* c, int which, int B) {
+  if (c->hnp != 3 || !c->sw.act_planes) return false;
+  const float* q = which == ACT_H1 ? c->h1 : which == ACT_CAT ? c->cat : c->cat2;
+  if (!act_twin(c, q).p) return false;
+  return gemm_h_ok_fwd_l2(c, which, B);
 }
 
 // Twin of a GEMM operand: a parameter (theta / target, while the parameter
@@ -727,16 +744,49 @@ static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int
 // ====================================================================== building blocks
 static const float* P(ddpg_ctx* c, const float* base, const Tensor& t) { return base + t.off; }
 
+// Every twin-GEMM reader of the activation `which` at batch B takes the twin
+// (act_planes_only): h1 -> actor layer 2 and dW2; cat -> critic hidden layer
+// and dWh; cat2 -> the critic hidden layer at (s, mu).
+static bool gemm_h_ok_fwd_l2(ddpg_ctx* c, int which, int B) {
+  const Layout& L = c->L;
+  int kh;
+  if (which == ACT_H1)
+    return gemm_h_ok<L_RK, L_KR>(c, c->h1, c->ldAH1, P(c, c->theta, L.a[AW2]), c->AH2, B, c->AH2,
+                                 c->AH1, 1, &kh) &&
+           gemm_h_ok<L_KR, L_KR>(c, c->h1, c->ldAH1, c->dz2, c->ldAH2, c->AH1, c->AH2, B, 0, &kh);
+  const float* q = which == ACT_CAT ? c->cat : c->cat2;
+  const bool fwd = gemm_h_ok<L_RK, L_KR>(c, q, c->ldC, P(c, c->theta, L.c[CWH]), c->CH2, B,
+                                         c->CH2, 2 * c->CH1, 1, &kh);
+  if (which == ACT_CAT2) return fwd;
+  return fwd && gemm_h_ok<L_KR, L_KR>(c, c->cat, c->ldC, c->dhp, c->ldCH2, 2 * c->CH1, c->CH2, B,
+                                      0, &kh);
+}
+
+// The EluGrad operand of a post-1 epilogue: the fp32 activation, or its planes
+// when only those were written.
+static void epi_aux(ddpg_ctx* c, GemmEpi& e, int which, int B, const float* q, int ld) {
+  e.ldaux = ld;
+  if (act_planes_only(c, which, B)) {
+    const Twin t = act_twin(c, q);
+    e.aux = nullptr;
+    e.auxh = t.p;
+    e.auxh_ps = t.ps;
+  } else {
+    e.aux = q;
+  }
+}
+
 // The actor's first layer as a thin-K part.  The target path's h1 is read only
 // by the next layer: when that runs on the twin GEMM, only the twin is written.
 static TkPart actor_l1_part(ddpg_ctx* c, const float* base, const float* s, int B, float* h1,
                             Twin* twin) {
   const Layout& L = c->L;
   int kh;
-  const Twin h1t = (h1 == c->th1 && gemm_h_ok<L_RK, L_KR>(c, h1, c->ldAH1, P(c, base, L.a[AW2]),
-                                                           c->AH2, B, c->AH2, c->AH1, 1, &kh))
-                       ? act_twin(c, h1)
-                       : Twin();
+  const bool planes = (h1 == c->th1 && gemm_h_ok<L_RK, L_KR>(c, h1, c->ldAH1,
+                                                             P(c, base, L.a[AW2]), c->AH2, B,
+                                                             c->AH2, c->AH1, 1, &kh)) ||
+                      (h1 == c->h1 && act_planes_only(c, ACT_H1, B));
+  const Twin h1t = planes ? act_twin(c, h1) : Twin();
   TkPart tp = tk_part(s, c->ldS, c->S, P(c, base, L.a[AW1]), c->AH1, 0, c->AH1,
                       P(c, base, L.a[AB1]), 1, h1t.p ? nullptr : h1, c->ldAH1);
   tp.outh = h1t.p;
@@ -796,10 +846,12 @@ static Twin critic_l1_parts(ddpg_ctx* c, const float* base, const float* s, cons
                             float* cat, TkPart tp[2]) {
   const Layout& L = c->L;
   int kh;
-  const Twin ct = (cat == c->tcat && gemm_h_ok<L_RK, L_KR>(c, cat, c->ldC, P(c, base, L.c[CWH]),
-                                                            c->CH2, B, c->CH2, 2 * c->CH1, 1, &kh))
-                      ? act_twin(c, cat)
-                      : Twin();
+  const bool planes =
+      (cat == c->tcat && gemm_h_ok<L_RK, L_KR>(c, cat, c->ldC, P(c, base, L.c[CWH]), c->CH2, B,
+                                                c->CH2, 2 * c->CH1, 1, &kh)) ||
+      (cat == c->cat && act_planes_only(c, ACT_CAT, B)) ||
+      (cat == c->cat2 && act_planes_only(c, ACT_CAT2, B));
+  const Twin ct = planes ? act_twin(c, cat) : Twin();
   tp[0] = tk_part(s, c->ldS, c->S, P(c, base, L.c[CWS]), c->CH1, 0, c->CH1, P(c, base, L.c[CBS]),
                   1, ct.p ? nullptr : cat, c->ldC);
   tp[1] = tk_part(a, c->ldA, c->A, P(c, base, L.c[CWA]), c->CH1, 0, c->CH1, P(c, base, L.c[CBA]),
@@ -893,8 +945,7 @@ static void critic_action_grad(ddpg_ctx* c, const float* s, const float* a, int 
   critic_fwd(c, c->theta, s, a, B, c->cat2, nullptr, 2, c->dhp2);
   GemmEpi e = epi_none();
   e.post = 1;
-  e.aux = c->cat2 + c->CH1;
-  e.ldaux = c->ldC;
+  epi_aux(c, e, ACT_CAT2, B, c->cat2 + c->CH1, c->ldC);
   e.proj = P(c, c->theta, L.c[CWA]);
   e.proj_n = c->A;
   e.proj_sn = 1;
@@ -1180,8 +1231,7 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
   e = epi_none();
   e.post = 1;
-  e.aux = c->cat;
-  e.ldaux = c->ldC;
+  epi_aux(c, e, ACT_CAT, B, c->cat, c->ldC);
   e.out = c->dcat;
   e.ldo = c->ldC;
   e.colsum = c->colpart;
@@ -1300,8 +1350,7 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   float* colpart1 = c->colpart + (size_t)mt2 * c->AH2;
   e = epi_none();
   e.post = 1;
-  e.aux = c->h1;
-  e.ldaux = c->ldAH1;
+  epi_aux(c, e, ACT_H1, B, c->h1, c->ldAH1);
   e.out = dz1t.p ? nullptr : c->dz1;
   e.outh = dz1t.p;
   e.h_plane_stride = dz1t.ps;
@@ -1749,6 +1798,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
       c->sw.l1_batch = !env_is("DDPG_L1BATCH", "0");
+      c->sw.act_planes = !env_is("DDPG_ACT32", "1");
     }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;

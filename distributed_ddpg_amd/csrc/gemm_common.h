@@ -67,6 +67,12 @@ struct GemmEpi {
   __bf16* outh;
   long long h_plane_stride;
   int h_planes;
+  // post 1 with auxh (and aux == nullptr): the EluGrad operand is read from
+  // its three exact bf16 planes ((h + m) + l == the fp32 value), offsets and
+  // ld as aux, planes auxh_ps apart -- for activations whose fp32 copy is not
+  // written (fp32 contexts whose other readers all take the twin)
+  const __bf16* auxh;
+  long long auxh_ps;
 };
 
 struct GemmArgs {
@@ -164,12 +170,22 @@ DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& 
       }
       float av[16];
       if constexpr (POST == 1) {  // all 16 loads in flight before the first use
+        if (e.auxh) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int n = ncol[NC == 1 ? 0 : (r >> 2) & 1];
-          const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
-          const float* q = (n < N && m < M) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
-          av[r] = *q;
+          for (int r = 0; r < 16; ++r) {
+            const int n = ncol[NC == 1 ? 0 : (r >> 2) & 1];
+            const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
+            const __bf16* q = e.auxh + ((n < N && m < M) ? (size_t)m * e.ldaux + n : 0);
+            av[r] = ((float)q[0] + (float)q[e.auxh_ps]) + (float)q[2 * e.auxh_ps];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int n = ncol[NC == 1 ? 0 : (r >> 2) & 1];
+            const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
+            const float* q = (n < N && m < M) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
+            av[r] = *q;
+          }
         }
       }
 #pragma unroll

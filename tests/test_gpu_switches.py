@@ -13,6 +13,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       summation order as the default 16x16x32 kernel)
     DDPG_L1BATCH=0    the large-batch step's first layers launched per network
                       instead of as one five-part thin_k launch
+    DDPG_ACT32=1      fp32 copies of h1 / cat / cat2 written beside their planes
+                      (the default reads the EluGrad operand from the planes)
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
     DDPG_GEMM=f32     every GEMM on the fp32-input MFMA kernel (no twins)
     DDPG_GEMM_H=0     no twins; large GEMMs on gemm_s3 (operands split while staging)
@@ -31,7 +33,8 @@ from test_gpu_parity import (CONFIGS, GRAD_TOL, FWD_TOL, _fill, _params, _sessio
 pytestmark = pytest.mark.gpu
 
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
-            "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH")
+            "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
+            "DDPG_ACT32")
 
 
 @pytest.fixture(scope="module")
@@ -114,6 +117,7 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_PAR", "1", "wide"),
     ("DDPG_SB_XCD", "0", "ip"),
     ("DDPG_L1BATCH", "0", "wide"),
+    ("DDPG_ACT32", "1", "wide"),
 ])
 def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
