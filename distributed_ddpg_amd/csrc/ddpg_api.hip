@@ -1862,8 +1862,13 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
                 {c->cat2, c->ldC, 2 * c->CH1}, {c->dhp, c->ldCH2, c->CH2},
                 {c->dhp2, c->ldCH2, c->CH2}, {c->dz2, c->ldAH2, c->AH2},
                 {c->dz1, c->ldAH1, c->AH1},  {c->dcat, c->ldC, 2 * c->CH1}};
-      for (const auto& t : tw)
+      for (const auto& t : tw) {
+        // dz1 / dcat are read as twins only by the dW1 / dWs GEMMs (M = S):
+        // below 128 state columns those never take the twin GEMM (and at
+        // S <= 64 they run on the skinny kernel), so no twin is written
+        if ((t.p == c->dz1 || t.p == c->dcat) && c->S < 128) continue;
         if (t.ld % 8 == 0 && t.w % 8 == 0) c->twinned.push_back({t.p, B * (size_t)t.ld});
+      }
     }
     HIP_TRY(hipMalloc(&c->d_slots, B * sizeof(int)));
     HIP_TRY(hipHostMalloc(&c->h_slots, kSlotRing * B * sizeof(int)));
