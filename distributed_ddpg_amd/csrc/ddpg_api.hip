@@ -224,6 +224,7 @@ struct ddpg_ctx {
   bool sb_shadow_ok = false;  // cleared by every theta write outside the small path
   size_t sb_smem = 0;         // dynamic LDS bytes of the phase kernels
   float* h_pred = nullptr;    // pinned [Bmax][A]: action-selection output (written by the GPU)
+  int td_nqt = 0;      // fused step: target-critic partials pending in qpart_t for critic_loss
   int sb_xstride = 0;  // XCD packing of the phase kernels: 0 auto (on up to 32 workgroups),
                        // env DDPG_SB_XCD=1 always (8), =0 never (1)
   unsigned long long* sb_stamps = nullptr;  // diagnostic (env DDPG_SB_STAMPS=1)
@@ -1165,9 +1166,21 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   {
     ProfScope ps(c, "critic_loss", 0, 0);
     // world > 1: the per-step stats are reduced over ranks below, then accumulated
+    // fused step: the TD target of ddpg.py:90-100 formed here (td_nqt)
+    TdTarget td;
+    memset(&td, 0, sizeof td);
+    if (fused && c->td_nqt > 0) {
+      td.qpart = c->qpart_t;
+      td.NT = c->td_nqt;
+      td.bo = P(c, c->target, L.c[CBO]);
+      td.r = c->r;
+      td.t = c->t;
+      td.gamma = c->cfg.gamma;
+    }
+    c->td_nqt = 0;
     hipLaunchKernelGGL(critic_loss_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->cur,
                        c->qpart, nq, B, P(c, c->theta, L.c[CBO]), c->y, inv_b, c->q, c->dq,
-                       c->lpart);
+                       c->lpart, td);
     HIP_TRY(hipGetLastError());
   }
   // column quads when the widths allow; dh_pre's twin is written here
@@ -1434,7 +1447,6 @@ static bool first_layers_dev(ddpg_ctx* c, int B) {
 }
 
 static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
-  const Layout& L = c->L;
   const hipStream_t s0 = c->cur;
   const hipStream_t s1 = c->par ? c->aux[0] : s0, s2 = c->par ? c->aux[1] : s0;
   // ddpg.py:90-109's batch-only first layers, all at once (every later use
@@ -1449,15 +1461,11 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   actor_fwd(c, c->target, c->s2, B, c->th1, nullptr, nullptr, c->ta2, l1);
   const int nqt =
       critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr, l1 ? 1 : 0);
-  {
-    ProfScope ps(c, "td_target", 0, 0);
-    hipLaunchKernelGGL(critic_q_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, c->cur, c->qpart,
-                       nqt, B, P(c, c->target, L.c[CBO]), nullptr, 1, c->r, c->t, c->cfg.gamma,
-                       c->y);
-    HIP_TRY(hipGetLastError());
-  }
   std::swap(c->ppart, c->ppart_t);
   std::swap(c->qpart, c->qpart_t);
+  // y = r + gamma (1 - t) Q'(s2, mu') is formed by the critic loss kernel from
+  // the target partials now in qpart_t (critic_train_dev, td_nqt)
+  c->td_nqt = nqt;
   // a_outs = actor.predict(s)  ddpg.py:106 (actor params are unchanged until actor.train)
   c->cur = s2;
   actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu, l1);

@@ -152,21 +152,43 @@ __global__ void critic_q_kernel(const float* __restrict__ qpart, int NT, int B,
 // 256 rows per block; each block leaves its {sum (y-q)^2, max q} partial in
 // lpart, and the critic-head kernel that runs next folds them (stats_fold).
 // inv_b is 1/B_global; the loss is this rank's share of the mean.
+// td (fused learner step): the TD target y = r + gamma (1 - t) Q'(s2, mu') of
+// critic_q_kernel mode 1 is formed here from the target critic's partials
+// (same sums, same ops) and stored to y, one launch fewer.
+struct TdTarget {
+  const float* qpart;  // target critic head partials, null: read y
+  int NT;
+  const float* bo;
+  const float* r;
+  const float* t;
+  float gamma;
+};
+
 __global__ __launch_bounds__(256) void critic_loss_kernel(
     const float* __restrict__ qpart, int NT, int B, const float* __restrict__ bo,
-    const float* __restrict__ y, float inv_b, float* __restrict__ q, float* __restrict__ dq,
-    float2* __restrict__ lpart) {
+    float* __restrict__ y, float inv_b, float* __restrict__ q, float* __restrict__ dq,
+    float2* __restrict__ lpart, TdTarget td) {
   __shared__ float s_sum[256];
   __shared__ float s_max[256];
   const int b = blockIdx.x * 256 + threadIdx.x;
   float lsum = 0.f, lmax = -INFINITY;
   if (b < B) {
+    float yb;
+    if (td.qpart) {
+      float zt = 0.f;
+      for (int tt = 0; tt < td.NT; ++tt) zt += td.qpart[(size_t)tt * B + b];
+      zt = __fadd_rn(zt, td.bo[0]);
+      yb = (td.t[b] != 0.f) ? td.r[b] : __fadd_rn(td.r[b], __fmul_rn(td.gamma, zt));
+      y[b] = yb;
+    } else {
+      yb = y[b];
+    }
     float z = 0.f;  // slab order; loads issued ahead of the adds
 #pragma unroll 8
     for (int tt = 0; tt < NT; ++tt) z += qpart[(size_t)tt * B + b];
     z = __fadd_rn(z, bo[0]);
     q[b] = z;
-    const float d = __fsub_rn(y[b], z);
+    const float d = __fsub_rn(yb, z);
     dq[b] = -__fmul_rn(inv_b, __fmul_rn(2.f, d));
     lsum = __fmul_rn(d, d);
     lmax = z;
