@@ -18,6 +18,7 @@
 #include "gemm_bf16.h"
 #include "gemm_s3.h"
 #include "gemm_h.h"
+#include "gemm_h256.h"
 #include "thin_k.h"
 #include "skinny.h"
 #include "kernels.h"
@@ -236,6 +237,7 @@ struct ddpg_ctx {
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
+    bool gemm256 = true;   // DDPG_GEMM256=0: no 256 x 256-tile bf16 GEMM (gemm_h256.h)
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
@@ -520,6 +522,30 @@ static bool gemm_h_ok(const ddpg_ctx* c, const float* A, int lda, const float* B
   return true;
 }
 
+// gemm_h256_kernel (bf16 configuration, 256 x 256 tiles): splits of a
+// weight gradient -- about one block per CU, every split a whole number of
+// the kernel's 4-step trips (kps % 128 == 0)
+static int h256_splits(int M, int N, int K, int cap) {
+  const int tiles = (M / H2_BM) * (N / H2_BN);
+  int sp = std::max(1, 256 / tiles);
+  sp = std::min(std::min(sp, cap), std::max(1, K / 128));
+  while (sp > 1 && (K % sp || (K / sp) % 128)) --sp;
+  return sp;
+}
+// -1: not taken; 0: split-K weight gradient with a plain slab epilogue;
+// 1: unsplit dX GEMM (post 1 epilogue) with >= 256 output tiles.  Full tiles
+// only.  env DDPG_GEMM256=0 keeps every bf16 GEMM on gemm_h16_kernel.
+static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e,
+                     bool dx_layout) {
+  if (!(c->hnp == 1 && c->sw.gemm256 && c->sw.gemm_mf == 16 && M % H2_BM == 0 &&
+        N % H2_BN == 0 && Kh % 128 == 0))
+    return -1;
+  const bool plain = !e.bias && e.act == 0 && e.post == 0 && !e.colsum && !e.proj_out && !e.outh;
+  if (splits != 1) return plain ? 0 : -1;
+  const bool dx = !e.bias && e.act == 0 && e.post == 1;
+  return dx && dx_layout && (M / H2_BM) * (N / H2_BN) >= 256 ? 1 : -1;
+}
+
 // direct: for a split-K weight gradient, where to write the result when the
 // plan ends up with one split (no slab, no reduction; plan.direct = true).
 template <int AL, int BL>
@@ -589,6 +615,38 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       a.xcd = xcd_rect(c, h.nt(N), h.mt(M), BMh, HG_BN);
       a.e = ee;
       static const char* lay[2] = {"RK", "KR"};
+      // bf16 configuration, whole 256 x 256 tiles (gemm_h256.h): the split-K
+      // weight gradients (plain slabs, MODE 0) and the dX GEMMs whose grid
+      // fills the chip unsplit (>= 256 tiles, MODE 1)
+      const int mode256 = h256_mode(c, M, N, Kh, splits, ee, AL == L_RK && BL == L_RK);
+      if (mode256 >= 0) {
+        GemmPlan q;
+        q.bm = q.bn = H2_BM;
+        const int sp = mode256 == 0 ? h256_splits(M, N, Kh, cap) : 1;
+        q.kps = Kh / sp;
+        q.splits = sp;
+        if (q.splits == 1 && direct) {
+          ee.out = direct;
+          ee.out_split_stride = 0;
+          q.direct = true;
+        }
+        a.e = ee;
+        a.kps = q.kps;
+        a.xcd = xcd_rect(c, q.nt(N), q.mt(M), H2_BM, H2_BN);
+        char key[112];
+        snprintf(key, sizeof key, "gemm_h256_kernel<%s,%s,MODE=%d>|%s", lay[AL], lay[BL], mode256,
+                 name);
+        ProfScope ps(c, key, 2.0 * M * N * (double)K,
+                     2.0 * ((double)M * K + (double)K * N) + 4.0 * (double)M * N * q.splits);
+        const dim3 grid(q.nt(N), q.mt(M), q.splits);
+        if (mode256 == 0) {
+          hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 0>), grid, dim3(H2_NT), 0, c->cur, a);
+        } else if constexpr (AL == L_RK && BL == L_RK) {
+          hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 1>), grid, dim3(H2_NT), 0, c->cur, a);
+        }
+        HIP_TRY(hipGetLastError());
+        return q;
+      }
       // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
       const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
       char key[112];
@@ -1802,6 +1860,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_s3 = !env_is("DDPG_GEMM", "f32");
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
+      c->sw.gemm256 = !env_is("DDPG_GEMM256", "0");
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
@@ -1814,6 +1873,13 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     c->split_cap_Ws = make_plan(c->S, c->CH1, c->Bmax, 0).splits;
     c->split_cap_Wa = make_plan(c->A, c->CH1, c->Bmax, 0).splits;
     c->split_cap_Wh = make_plan(2 * c->CH1, c->CH2, c->Bmax, 0).splits;
+    if (c->cfg.dtype == DDPG_BF16) {  // the 256 x 256-tile kernel splits finer
+      auto cap256 = [&](int M, int N) {
+        return (M % H2_BM || N % H2_BN) ? 1 : std::max(1, 256 / ((M / H2_BM) * (N / H2_BN)));
+      };
+      c->split_cap_W2 = std::max(c->split_cap_W2, cap256(c->AH1, c->AH2));
+      c->split_cap_Wh = std::max(c->split_cap_Wh, cap256(2 * c->CH1, c->CH2));
+    }
     struct Req {
       float** p;
       size_t n;

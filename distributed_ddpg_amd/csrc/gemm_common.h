@@ -150,7 +150,8 @@ DDPG_DEV int acc_col(int r, int lane) {
 // on the flag combinations the learner uses (BIAS: + bias[n]; ACT 1: elu;
 // POST 1: * EluGrad factor of aux[m][n]; POST 2: pw[n] * EluGrad factor of v).
 // Values outside the M x N range become 0 (they feed the row reductions).
-template <int BM, int BN, int WGN, bool BIAS, int ACT, int POST, int MF>
+// FULL: the tile lies inside M x N (the caller checked), no range tests.
+template <int BM, int BN, int WGN, bool BIAS, int ACT, int POST, int MF, bool FULL = false>
 DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& e, int M, int N,
                         int n0, int m0, int wm, int wn, int lane) {
   constexpr int TM = BM / 64, TN = BN / (32 * WGN);
@@ -165,8 +166,8 @@ DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& 
 #pragma unroll
       for (int u = 0; u < NC; ++u) {
         ncol[u] = n0 + wn * WC + j * 32 + acc_col<MF>(4 * u, lane);
-        bnc[u] = (BIAS && ncol[u] < N) ? e.bias[ncol[u]] : 0.f;
-        pwc[u] = (POST == 2 && ncol[u] < N) ? e.pw[ncol[u]] : 0.f;
+        bnc[u] = (BIAS && (FULL || ncol[u] < N)) ? e.bias[ncol[u]] : 0.f;
+        pwc[u] = (POST == 2 && (FULL || ncol[u] < N)) ? e.pw[ncol[u]] : 0.f;
       }
       float av[16];
       if constexpr (POST == 1) {  // all 16 loads in flight before the first use
@@ -175,7 +176,7 @@ DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& 
           for (int r = 0; r < 16; ++r) {
             const int n = ncol[NC == 1 ? 0 : (r >> 2) & 1];
             const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
-            const __bf16* q = e.auxh + ((n < N && m < M) ? (size_t)m * e.ldaux + n : 0);
+            const __bf16* q = e.auxh + ((FULL || (n < N && m < M)) ? (size_t)m * e.ldaux + n : 0);
             av[r] = ((float)q[0] + (float)q[e.auxh_ps]) + (float)q[2 * e.auxh_ps];
           }
         } else {
@@ -183,7 +184,7 @@ DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& 
           for (int r = 0; r < 16; ++r) {
             const int n = ncol[NC == 1 ? 0 : (r >> 2) & 1];
             const int m = m0 + wm * WR + i * 32 + acc_row<MF>(r, lane);
-            const float* q = (n < N && m < M) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
+            const float* q = (FULL || (n < N && m < M)) ? e.aux + (size_t)m * e.ldaux + n : e.aux;
             av[r] = *q;
           }
         }
@@ -200,7 +201,7 @@ DDPG_DEV void epi_apply(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], const GemmEpi& 
         if constexpr (ACT == 1) v = elu_f(v);
         if constexpr (POST == 1) v = __fmul_rn(v, elu_grad_factor(av[r]));
         if constexpr (POST == 2) v = __fmul_rn(pwn, elu_grad_factor(v));
-        acc[i][j][r] = (nok && m < M) ? v : 0.f;
+        acc[i][j][r] = (FULL || (nok && m < M)) ? v : 0.f;
       }
     }
   }
@@ -221,7 +222,14 @@ DDPG_DEV void store_twin(const GemmEpi& e, size_t i, float4 v) {
 // wave row (BM/2 rows) at a time, from where it is stored as float4 rows
 // (1 KiB per wave instruction instead of 128-B column pieces) and reduced
 // (bias-gradient column sums, thin projections).
-template <int BM, int BN, int WGN = 2, int MF = 32>
+// PR: tile rows staged through LDS per pass (default BM / 2, one wave row;
+// BM / 4 for the 256 x 256 tile of gemm_h256.h, whose full wave row would not
+// fit beside the projection weights): smem must hold
+// PR * (BN + 4) + BN * PROJ_MAX + 2 * GNT floats.
+// ONLY >= 0: compile just that element-wise variant (the order of the
+// dispatch below; the caller guarantees the flags), fewer live registers.
+template <int BM, int BN, int WGN = 2, int MF = 32, int PR = BM / 2, bool FULL = false,
+          int ONLY = -1>
 DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem,
                             const GemmArgs& g,
                             int tid, int n0, int m0, int z, int bx, int by) {
@@ -229,6 +237,8 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   constexpr int NT = 2 * WGN * 64;  // threads
   constexpr int TM = BM / 64, TN = BN / (32 * WGN);
   constexpr int WR = BM / 2, WC = BN / WGN;
+  constexpr int PPW = WR / PR;  // passes per wave row
+  static_assert(PR <= WR && WR % PR == 0 && PR % 32 == 0, "pass rows");
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WGN, wn = wave % WGN;
   const GemmEpi& e = g.e;
@@ -236,30 +246,34 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   float* outp = e.out ? e.out + (size_t)z * e.out_split_stride : nullptr;
 
   const bool bias = e.bias != nullptr;
-  if (!bias && e.act == 0 && e.post == 0)
-    epi_apply<BM, BN, WGN, false, 0, 0, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
+  if constexpr (ONLY == 0)
+    epi_apply<BM, BN, WGN, false, 0, 0, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
+  else if constexpr (ONLY == 3)
+    epi_apply<BM, BN, WGN, false, 0, 1, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
+  else if (!bias && e.act == 0 && e.post == 0)
+    epi_apply<BM, BN, WGN, false, 0, 0, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (bias && e.act == 1 && e.post == 0)
-    epi_apply<BM, BN, WGN, true, 1, 0, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
+    epi_apply<BM, BN, WGN, true, 1, 0, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (bias && e.act == 1 && e.post == 2)
-    epi_apply<BM, BN, WGN, true, 1, 2, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
+    epi_apply<BM, BN, WGN, true, 1, 2, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (!bias && e.act == 0 && e.post == 1)
-    epi_apply<BM, BN, WGN, false, 0, 1, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
+    epi_apply<BM, BN, WGN, false, 0, 1, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (bias && e.act == 0 && e.post == 0)
-    epi_apply<BM, BN, WGN, true, 0, 0, MF>(acc, e, M, N, n0, m0, wm, wn, lane);
+    epi_apply<BM, BN, WGN, true, 0, 0, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else  // not used by the learner; the host rejects other combinations
     __builtin_trap();
 
   if (!outp && !e.outh && !e.colsum && !e.proj_out) return;
 
   constexpr int VS_LD = TC::VS_LD;
-  float* Vs = smem;                      // [WR][VS_LD]
-  float* Wps = smem + WR * VS_LD;        // [BN][PN]
+  float* Vs = smem;                      // [PR][VS_LD]
+  float* Wps = smem + PR * VS_LD;        // [BN][PN]
   float* red = Wps + BN * PROJ_MAX;      // [NT]
   const int PN = (e.proj_n + 3) & ~3;
   if (e.proj_out) {
     for (int idx = tid; idx < BN * PN; idx += NT) {
       const int nl = idx / PN, a = idx - nl * PN, n = n0 + nl;
-      Wps[idx] = (n < N && a < e.proj_n) ? e.proj[(size_t)n * e.proj_sn + (size_t)a * e.proj_sa]
+      Wps[idx] = ((FULL || n < N) && a < e.proj_n) ? e.proj[(size_t)n * e.proj_sn + (size_t)a * e.proj_sa]
                                           : 0.f;
     }
   }
@@ -275,29 +289,32 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
                    BN % 8 == 0 && NT % (BN / 8) == 0;
   constexpr int CG = NT / BN;  // column-sum row groups
   float csum = 0.f;
+  // one LDS pass of PR rows (unrolled: a runtime pass index sends the
+  // accumulators to scratch)
+  auto do_pass = [&](int pass) {
+    if (wm == pass / PPW) {
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        if ((i * 32) / PR != pass % PPW) continue;  // this pass's 32-row blocks
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int rl = i * 32 + acc_row<MF>(r, lane);
+            const int rl = i * 32 - (pass % PPW) * PR + acc_row<MF>(r, lane);
             Vs[rl * VS_LD + wn * WC + j * 32 + acc_col<MF>(r, lane)] = acc[i][j][r];
           }
+      }
     }
     __syncthreads();
     if ((outp || e.outh) && oct) {
       // 8 columns per thread: 16-B stores for the fp32 rows and every twin plane
       constexpr int C8 = BN / 8, RPR8 = NT / C8;
       const int c8 = tid % C8, rr0 = tid / C8, n = n0 + 8 * c8;
-      if (n < N) {
+      if (FULL || n < N) {
 #pragma unroll 2
-        for (int rr = rr0; rr < WR; rr += RPR8) {
-          const int m = m0 + pass * WR + rr;
-          if (m >= M) continue;
+        for (int rr = rr0; rr < PR; rr += RPR8) {
+          const int m = m0 + pass * PR + rr;
+          if (!FULL && m >= M) continue;
           const float4 va = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 8 * c8);
           const float4 vb = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 8 * c8 + 4);
           const size_t o = (size_t)m * e.ldo + n;
@@ -313,8 +330,8 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
     } else if (outp || e.outh) {
       const int c4 = tid % C4, rr0 = tid / C4, n = n0 + 4 * c4;
 #pragma unroll 4
-      for (int rr = rr0; rr < WR; rr += RPR) {
-        const int m = m0 + pass * WR + rr;
+      for (int rr = rr0; rr < PR; rr += RPR) {
+        const int m = m0 + pass * PR + rr;
         if (m < M) {
           const float4 v = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 4 * c4);
           float* o = outp ? outp + (size_t)m * e.ldo + n : nullptr;
@@ -334,12 +351,12 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
     if (e.colsum) {
       const int col = tid % BN, grp = tid / BN;
 #pragma unroll 4
-      for (int rr = grp; rr < WR; rr += CG) csum += Vs[rr * VS_LD + col];
+      for (int rr = grp; rr < PR; rr += CG) csum += Vs[rr * VS_LD + col];
     }
     if (e.proj_out) {
       const int PG = PN >> 2;
-      for (int p = tid; p < WR * PG; p += NT) {
-        const int row = p % WR, ag = p / WR;
+      for (int p = tid; p < PR * PG; p += NT) {
+        const int row = p % PR, ag = p / PR;
         float4 ap = make_float4(0.f, 0.f, 0.f, 0.f);
         // partial unroll: a full unroll makes every Wps load invariant in p
         // and the compiler hoists them all into registers (spills at BN=64)
@@ -356,8 +373,8 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
             ap.w = fmaf(vq[q], w.w, ap.w);
           }
         }
-        const int m = m0 + pass * WR + row;
-        if (m < M) {
+        const int m = m0 + pass * PR + row;
+        if (FULL || m < M) {
           float* po = e.proj_out + ((size_t)bx * M + m) * e.proj_n;
           const float av[4] = {ap.x, ap.y, ap.z, ap.w};
 #pragma unroll
@@ -367,7 +384,9 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
       }
     }
     __syncthreads();
-  }
+  };
+#pragma unroll
+  for (int pass = 0; pass < 2 * PPW; ++pass) do_pass(pass);
   if (e.colsum) {
     red[tid] = csum;
     __syncthreads();
@@ -376,7 +395,7 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
 #pragma unroll
       for (int gi = 0; gi < CG; ++gi) s += red[tid + gi * BN];
       const int n = n0 + tid;
-      if (n < N) e.colsum[((size_t)z * gridDim.y + by) * e.ld_colsum + n] = s;
+      if (FULL || n < N) e.colsum[((size_t)z * gridDim.y + by) * e.ld_colsum + n] = s;
     }
   }
 }

@@ -21,6 +21,10 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_THINK=0      the K <= 64 layers on the tiled GEMMs instead of thin_k
     DDPG_SKINNY=0     the <= 64-wide weight gradients on the GEMMs instead of
                       the skinny VALU kernel
+  bf16 configuration, different summation order -- the oracle's bf16 bars,
+  and the two paths' gradients against each other:
+    DDPG_GEMM256=0    no 256 x 256-tile GEMM (gemm_h256.h): the split-K weight
+                      gradients and the >= 256-tile dX GEMMs on gemm_h16_kernel
 """
 import random
 
@@ -34,7 +38,7 @@ pytestmark = pytest.mark.gpu
 
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
-            "DDPG_ACT32")
+            "DDPG_ACT32", "DDPG_GEMM256")
 
 
 @pytest.fixture(scope="module")
@@ -141,6 +145,38 @@ def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
     assert any(k.startswith("gemm_h_kernel") and "NP=1" in k for k in got["keys"]), got["keys"]
     assert not any(k.startswith("gemm_h16_kernel") for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
+
+
+def test_gemm256_switch_bf16(dd, O, monkeypatch):
+    """bf16 configuration at the 1024-wide config (B = 256): the split-K
+    weight gradients dWh (2048 x 1024) and dW2 (1024 x 1024) run on
+    gemm_h256_kernel (MODE 0, whole 256 x 256 tiles) by default and on
+    gemm_h16_kernel with DDPG_GEMM256=0.  The products are the same bf16
+    values with fp32 accumulation in another order: the first step's
+    gradients agree to 1e-5 norm-wise, and both runs' parameters after 3
+    fused steps meet the oracle's stated bf16 bar (BF16_PARAM_TOL)."""
+    from test_gpu_parity import BF16_PARAM_TOL, normrel
+    _clear(monkeypatch)
+    name = "wide"
+    p, _ = _params(O, name)
+    ref1 = _run(dd, O, name, p, 1, dtype="bf16")
+    ref = _run(dd, O, name, p, 3, dtype="bf16", profile=True)
+    assert "gemm_h256_kernel<KR,KR,MODE=0>|wgrad" in ref["keys"], ref["keys"]
+    monkeypatch.setenv("DDPG_GEMM256", "0")
+    got1 = _run(dd, O, name, p, 1, dtype="bf16")
+    got = _run(dd, O, name, p, 3, dtype="bf16", profile=True)
+    assert not any(k.startswith("gemm_h256_kernel") for k in got["keys"]), got["keys"]
+    assert any(k.startswith("gemm_h16_kernel<KR,KR") for k in got["keys"]), got["keys"]
+    # first-step gradients (same parameters in): summation order only
+    for x, y in zip(ref1["state"][8:], got1["state"][8:]):
+        for u, v in zip(x, y):
+            assert normrel(v, u) < 1e-5, normrel(v, u)
+    L, _ = _oracle(O, name, p, ref["rows"], 3)
+    for run in (ref, got):
+        for (net, keys), vals in zip((("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS)),
+                                     run["state"][:2]):
+            for k, v in zip(keys, vals):
+                assert rel(v, L.state()[net][k].reshape(v.shape)) < BF16_PARAM_TOL, (net, k)
 
 
 @pytest.mark.parametrize("switch,value,kernel,absent", [

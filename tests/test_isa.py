@@ -10,6 +10,7 @@ twin GEMM was exactly that (profiles/r3/np3_h16_fault_cause.txt); a variant
 like it now fails here, at build time, instead of on the GPU.
 Host only: reads the .so, runs nothing on a GPU."""
 import os
+import re
 import sys
 
 import pytest
@@ -41,8 +42,25 @@ def test_every_gemm_and_thin_k_kernel_is_covered(isa):
     assert any("gemm_h_kernel" in n for n in names)
     assert any("gemm_h16_kernel" in n for n in names)
     assert any("thin_k_kernel" in n for n in names)
+    assert any("gemm_h256_kernel" in n for n in names)
+    dis = isa.disassemble(co)
     for n in names:
-        assert res[n].get("scratch", -1) == 0, n
+        if re.search(isa.EPILOGUE_SPILL_OK, n):
+            # allowed epilogue spills only: none inside the MFMA main loop
+            assert not isa._scratch_in_main_loop(dis[n]), n
+        else:
+            assert res[n].get("scratch", -1) == 0, n
+
+
+def test_buffer_load_lds_has_no_vgpr_destination(isa):
+    """buffer_load ... lds (LDS-DMA) writes LDS; its VGPR operand is the
+    address, so reading / rewriting that VGPR before the DMA lands is fine."""
+    insns = [
+        (0x0, "buffer_load_dwordx4", "v196, s[0:3], 0 offen lds", None),
+        (0x8, "v_add_u32_e32", "v196, 0x40, v196", None),
+        (0x10, "s_endpgm", "", None),
+    ]
+    assert isa.scan_kernel(insns) == []
 
 
 def test_hazard_scan_catches_async_return_clobber(isa):
