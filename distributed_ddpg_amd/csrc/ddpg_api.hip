@@ -237,7 +237,7 @@ struct ddpg_ctx {
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
-    bool gemm256 = true;   // DDPG_GEMM256=0: no 256 x 256-tile bf16 GEMM (gemm_h256.h)
+    int gemm256 = 1;       // DDPG_GEMM256=0: no 256 x 256-tile bf16 GEMM (gemm_h256.h); 2: also the 128-tile forwards
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
@@ -536,14 +536,18 @@ static int h256_splits(int M, int N, int K, int cap) {
 // 1: unsplit dX GEMM (post 1 epilogue) with >= 256 output tiles.  Full tiles
 // only.  env DDPG_GEMM256=0 keeps every bf16 GEMM on gemm_h16_kernel.
 static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e,
-                     bool dx_layout) {
+                     bool dx_layout, bool a_rk) {
   if (!(c->hnp == 1 && c->sw.gemm256 && c->sw.gemm_mf == 16 && M % H2_BM == 0 &&
         N % H2_BN == 0 && Kh % 128 == 0))
     return -1;
   const bool plain = !e.bias && e.act == 0 && e.post == 0 && !e.colsum && !e.proj_out && !e.outh;
   if (splits != 1) return plain ? 0 : -1;
   const bool dx = !e.bias && e.act == 0 && e.post == 1;
-  return dx && dx_layout && (M / H2_BM) * (N / H2_BN) >= 256 ? 1 : -1;
+  const int tiles = (M / H2_BM) * (N / H2_BN);
+  if (dx && dx_layout && tiles >= 256) return 1;
+  // DDPG_GEMM256=2 (measurement switch): every unsplit GEMM of >= 128 tiles,
+  // relying on the step's concurrent streams to fill the chip
+  return c->sw.gemm256 == 2 && a_rk && tiles >= 128 ? 2 : -1;
 }
 
 // direct: for a split-K weight gradient, where to write the result when the
@@ -618,7 +622,7 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       // bf16 configuration, whole 256 x 256 tiles (gemm_h256.h): the split-K
       // weight gradients (plain slabs, MODE 0) and the dX GEMMs whose grid
       // fills the chip unsplit (>= 256 tiles, MODE 1)
-      const int mode256 = h256_mode(c, M, N, Kh, splits, ee, AL == L_RK && BL == L_RK);
+      const int mode256 = h256_mode(c, M, N, Kh, splits, ee, AL == L_RK && BL == L_RK, AL == L_RK);
       if (mode256 >= 0) {
         GemmPlan q;
         q.bm = q.bn = H2_BM;
@@ -641,6 +645,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
         const dim3 grid(q.nt(N), q.mt(M), q.splits);
         if (mode256 == 0) {
           hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 0>), grid, dim3(H2_NT), 0, c->cur, a);
+        } else if (mode256 == 2) {
+          if constexpr (AL == L_RK)
+            hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 2>), grid, dim3(H2_NT), 0, c->cur, a);
         } else if constexpr (AL == L_RK && BL == L_RK) {
           hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 1>), grid, dim3(H2_NT), 0, c->cur, a);
         }
@@ -1860,7 +1867,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_s3 = !env_is("DDPG_GEMM", "f32");
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
-      c->sw.gemm256 = !env_is("DDPG_GEMM256", "0");
+      c->sw.gemm256 = env_is("DDPG_GEMM256", "0") ? 0 : env_is("DDPG_GEMM256", "2") ? 2 : 1;
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");

@@ -86,7 +86,8 @@ DDPG_DEV void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); 
 
 // MODE 1: fused epilogue (gemm_common.h) of the dX GEMMs (no bias, no
 // activation, EluGrad factor of aux: post 1; column sums, projection, twin),
-// one split.  MODE 0: split-K weight
+// one split.  MODE 2: any epilogue the learner uses (runtime dispatch), one
+// split.  MODE 0: split-K weight
 // gradients: each split stores its fp32 slab (out + z * out_split_stride)
 // straight from the registers, nothing else.  Full tiles only (the host
 // checks M % 256 == N % 256 == 0 and kps % 128 == 0).
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(H2_NT, 1) void gemm_h256_kernel(GemmHArgs g) {
         for (int tc = 0; tc < 2; ++tc)
 #pragma unroll
           for (int q = 0; q < 4; ++q) out[I][J][4 * (2 * tr + tc) + q] = acc[2 * I + tr][2 * J + tc][q];
-  gemm_epilogue<256, 256, 4, 16, 64, true, 3>(out, smem, ge, tid, n0, m0, 0, bx, by);
+  gemm_epilogue<256, 256, 4, 16, 64, true, MODE == 1 ? 3 : -1>(out, smem, ge, tid, n0, m0, 0, bx, by);
 }
 
 }  // namespace ddpg

@@ -46,7 +46,7 @@ def test_every_gemm_and_thin_k_kernel_is_covered(isa):
     dis = isa.disassemble(co)
     for n in names:
         if re.search(isa.EPILOGUE_SPILL_OK, n):
-            # allowed epilogue spills only: none inside the MFMA main loop
+            # allowed epilogue spills only: no scratch load inside the MFMA main loop
             assert not isa._scratch_in_main_loop(dis[n]), n
         else:
             assert res[n].get("scratch", -1) == 0, n
