@@ -237,7 +237,7 @@ struct ddpg_ctx {
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
-    int gemm256 = 1;       // DDPG_GEMM256=0: no 256 x 256-tile bf16 GEMM (gemm_h256.h); 2: also the 128-tile forwards
+    int gemm256 = 1;       // DDPG_GEMM256=0: no 256 x 256-tile bf16 GEMM (gemm_h256.h); 2, 3: more shapes
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
@@ -532,8 +532,8 @@ static int h256_splits(int M, int N, int K, int cap) {
   while (sp > 1 && (K % sp || (K / sp) % 128)) --sp;
   return sp;
 }
-// -1: not taken; 0: split-K weight gradient with a plain slab epilogue;
-// 1: unsplit dX GEMM (post 1 epilogue) with >= 256 output tiles.  Full tiles
+// -1: not taken; 0: split-K weight gradient with a plain slab epilogue (the
+// default); 1 / 2: unsplit GEMMs (measurement switches below).  Full tiles
 // only.  env DDPG_GEMM256=0 keeps every bf16 GEMM on gemm_h16_kernel.
 static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e,
                      bool dx_layout, bool a_rk) {
@@ -542,12 +542,13 @@ static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const 
     return -1;
   const bool plain = !e.bias && e.act == 0 && e.post == 0 && !e.colsum && !e.proj_out && !e.outh;
   if (splits != 1) return plain ? 0 : -1;
+  // measurement switches (same-box A/B): DDPG_GEMM256=2 adds the
+  // >= 256-tile dX GEMMs (MODE 1); 3 also every unsplit GEMM of >= 128 tiles
+  // (MODE 2, relying on the step's concurrent streams to fill the chip)
   const bool dx = !e.bias && e.act == 0 && e.post == 1;
   const int tiles = (M / H2_BM) * (N / H2_BN);
-  if (dx && dx_layout && tiles >= 256) return 1;
-  // DDPG_GEMM256=2 (measurement switch): every unsplit GEMM of >= 128 tiles,
-  // relying on the step's concurrent streams to fill the chip
-  return c->sw.gemm256 == 2 && a_rk && tiles >= 128 ? 2 : -1;
+  if (c->sw.gemm256 >= 2 && dx && dx_layout && tiles >= 256) return 1;
+  return c->sw.gemm256 == 3 && a_rk && tiles >= 128 ? 2 : -1;
 }
 
 // direct: for a split-K weight gradient, where to write the result when the
@@ -589,6 +590,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
     const int BKh = c->hnp == 1 ? 64 : 32, BMh = c->hnp == 1 ? 256 : 128;
     const Twin ta = operand_twin(c, A), tb = operand_twin(c, B);
     {
+      // as requested (the 256 x 128 plan below rewrites both)
+      const int splits_req = splits;  // 1: plain GEMM; otherwise a split-K weight gradient
+      const GemmEpi ee_req = ee;
       GemmPlan h;
       h.bm = BMh;
       h.bn = HG_BN;
@@ -622,19 +626,21 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       // bf16 configuration, whole 256 x 256 tiles (gemm_h256.h): the split-K
       // weight gradients (plain slabs, MODE 0) and the dX GEMMs whose grid
       // fills the chip unsplit (>= 256 tiles, MODE 1)
-      const int mode256 = h256_mode(c, M, N, Kh, splits, ee, AL == L_RK && BL == L_RK, AL == L_RK);
+      const int mode256 =
+          h256_mode(c, M, N, Kh, splits_req, ee_req, AL == L_RK && BL == L_RK, AL == L_RK);
       if (mode256 >= 0) {
         GemmPlan q;
         q.bm = q.bn = H2_BM;
         const int sp = mode256 == 0 ? h256_splits(M, N, Kh, cap) : 1;
         q.kps = Kh / sp;
         q.splits = sp;
+        GemmEpi e2 = ee_req;
         if (q.splits == 1 && direct) {
-          ee.out = direct;
-          ee.out_split_stride = 0;
+          e2.out = direct;
+          e2.out_split_stride = 0;
           q.direct = true;
         }
-        a.e = ee;
+        a.e = e2;
         a.kps = q.kps;
         a.xcd = xcd_rect(c, q.nt(N), q.mt(M), H2_BM, H2_BN);
         char key[112];
@@ -1867,7 +1873,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_s3 = !env_is("DDPG_GEMM", "f32");
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
-      c->sw.gemm256 = env_is("DDPG_GEMM256", "0") ? 0 : env_is("DDPG_GEMM256", "2") ? 2 : 1;
+      if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = std::min(3, std::max(0, atoi(v)));
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
