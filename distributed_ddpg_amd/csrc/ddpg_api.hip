@@ -237,7 +237,7 @@ struct ddpg_ctx {
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
-    int gemm256 = 1;       // DDPG_GEMM256=0: no 256 x 256-tile bf16 GEMM (gemm_h256.h); 2, 3: more shapes
+    int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h; 2, 3: more shapes
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
@@ -532,9 +532,10 @@ static int h256_splits(int M, int N, int K, int cap) {
   while (sp > 1 && (K % sp || (K / sp) % 128)) --sp;
   return sp;
 }
-// -1: not taken; 0: split-K weight gradient with a plain slab epilogue (the
-// default); 1 / 2: unsplit GEMMs (measurement switches below).  Full tiles
-// only.  env DDPG_GEMM256=0 keeps every bf16 GEMM on gemm_h16_kernel.
+// -1: not taken; 0: split-K weight gradient with a plain slab epilogue
+// (DDPG_GEMM256=1); 1 / 2: unsplit GEMMs (=2 / =3).  Full tiles only.  Off by
+// default: in the C5 step the finer split's extra slab reduction cost more
+// than the faster main loop saved (profiles/r3/gemm_h256_ab_c5.txt).
 static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e,
                      bool dx_layout, bool a_rk) {
   if (!(c->hnp == 1 && c->sw.gemm256 && c->sw.gemm_mf == 16 && M % H2_BM == 0 &&

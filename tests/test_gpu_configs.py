@@ -270,8 +270,6 @@ def test_c5_bf16_full_dims(dd, O):
     prof.enable(False)
     assert any((k.startswith("gemm_s3_kernel") and "NP=1" in k) or
                (k.startswith("gemm_h") and "NP=1" in k) for k in keys), sorted(keys)
-    # the 256 x 256-tile GEMM: the two large weight gradients dWh, dW2 (MODE 0)
-    assert "gemm_h256_kernel<KR,KR,MODE=0>|wgrad" in keys, sorted(keys)
     idx = np.array(random.Random(1234).sample(range(6000), B))
     L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
     out = L.step(*(x[idx] for x in rows))

@@ -23,8 +23,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       the skinny VALU kernel
   bf16 configuration, different summation order -- the oracle's bf16 bars,
   and the two paths' gradients against each other:
-    DDPG_GEMM256=0    no 256 x 256-tile GEMM (gemm_h256.h): the split-K weight
-                      gradients and the >= 256-tile dX GEMMs on gemm_h16_kernel
+    DDPG_GEMM256=1    the split-K weight gradients on the 256 x 256-tile GEMM
+                      (gemm_h256.h) instead of gemm_h16_kernel
 """
 import random
 
@@ -148,29 +148,30 @@ def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
 
 
 def test_gemm256_switch_bf16(dd, O, monkeypatch):
-    """bf16 configuration at the 1024-wide config (B = 256): the split-K
-    weight gradients dWh (2048 x 1024) and dW2 (1024 x 1024) run on
-    gemm_h256_kernel (MODE 0, whole 256 x 256 tiles) by default and on
-    gemm_h16_kernel with DDPG_GEMM256=0.  The products are the same bf16
-    values with fp32 accumulation in another order: the first step's
-    gradients agree to 1e-5 norm-wise, and both runs' parameters after 3
-    fused steps meet the oracle's stated bf16 bar (BF16_PARAM_TOL)."""
+    """bf16 configuration at the 1024-wide config (B = 256): with
+    DDPG_GEMM256=1 the split-K weight gradients dWh (2048 x 1024) and dW2
+    (1024 x 1024) run on gemm_h256_kernel (MODE 0, whole 256 x 256 tiles); by
+    default (measured slower in the step) on gemm_h16_kernel.  The
+    products are the same bf16 values with fp32 accumulation in another
+    order: the first step's critic gradients agree to 1e-5 norm-wise (the
+    actor's, taken through the UPDATED critic whose Adam step can flip on
+    near-zero gradients, to 1e-3), and both runs' parameters after 3 fused
+    steps meet the oracle's stated bf16 bar (BF16_PARAM_TOL)."""
     from test_gpu_parity import BF16_PARAM_TOL, normrel
     _clear(monkeypatch)
     name = "wide"
     p, _ = _params(O, name)
     ref1 = _run(dd, O, name, p, 1, dtype="bf16")
     ref = _run(dd, O, name, p, 3, dtype="bf16", profile=True)
-    assert "gemm_h256_kernel<KR,KR,MODE=0>|wgrad" in ref["keys"], ref["keys"]
-    monkeypatch.setenv("DDPG_GEMM256", "0")
+    assert not any(k.startswith("gemm_h256_kernel") for k in ref["keys"]), ref["keys"]
+    assert any(k.startswith("gemm_h16_kernel<KR,KR") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_GEMM256", "1")
     got1 = _run(dd, O, name, p, 1, dtype="bf16")
     got = _run(dd, O, name, p, 3, dtype="bf16", profile=True)
-    assert not any(k.startswith("gemm_h256_kernel") for k in got["keys"]), got["keys"]
-    assert any(k.startswith("gemm_h16_kernel<KR,KR") for k in got["keys"]), got["keys"]
-    # first-step gradients (same parameters in): summation order only
-    for x, y in zip(ref1["state"][8:], got1["state"][8:]):
+    assert "gemm_h256_kernel<KR,KR,MODE=0>|wgrad" in got["keys"], got["keys"]
+    for bar, x, y in zip((1e-3, 1e-5), ref1["state"][8:], got1["state"][8:]):  # actor, critic
         for u, v in zip(x, y):
-            assert normrel(v, u) < 1e-5, normrel(v, u)
+            assert normrel(v, u) < bar, normrel(v, u)
     L, _ = _oracle(O, name, p, ref["rows"], 3)
     for run in (ref, got):
         for (net, keys), vals in zip((("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS)),
