@@ -19,6 +19,7 @@
 #include "gemm_s3.h"
 #include "gemm_h.h"
 #include "gemm_h256.h"
+#include "gemm_h3.h"
 #include "thin_k.h"
 #include "skinny.h"
 #include "kernels.h"
@@ -237,7 +238,8 @@ struct ddpg_ctx {
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
-    int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h; 2, 3: more shapes
+    bool gemm_h3 = true;   // DDPG_GEMM_H3=0: fp32 twin GEMM on gemm_h_kernel (runtime slot addressing)
+    int gemm256 = 0;       // DDPG_GEMM256=1 / 4: bf16 split-K weight gradients on gemm_h256.h; 2, 3: more shapes
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
@@ -548,7 +550,7 @@ static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const 
   // (MODE 2, relying on the step's concurrent streams to fill the chip)
   const bool dx = !e.bias && e.act == 0 && e.post == 1;
   const int tiles = (M / H2_BM) * (N / H2_BN);
-  if (c->sw.gemm256 >= 2 && dx && dx_layout && tiles >= 256) return 1;
+  if ((c->sw.gemm256 == 2 || c->sw.gemm256 == 3) && dx && dx_layout && tiles >= 256) return 1;
   return c->sw.gemm256 == 3 && a_rk && tiles >= 128 ? 2 : -1;
 }
 
@@ -632,7 +634,11 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       if (mode256 >= 0) {
         GemmPlan q;
         q.bm = q.bn = H2_BM;
-        const int sp = mode256 == 0 ? h256_splits(M, N, Kh, cap) : 1;
+        int sp = mode256 == 0 ? h256_splits(M, N, Kh, cap) : 1;
+        // DDPG_GEMM256=4: the 256 x 128 plan's split count (no extra slab to
+        // reduce; half the blocks, beside the concurrent dX chain)
+        if (mode256 == 0 && c->sw.gemm256 == 4 && Kh % h.splits == 0 && (Kh / h.splits) % 128 == 0)
+          sp = h.splits;
         q.kps = Kh / sp;
         q.splits = sp;
         GemmEpi e2 = ee_req;
@@ -664,7 +670,8 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
       const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
       char key[112];
-      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s", h16 ? "gemm_h16_kernel" : "gemm_h_kernel",
+      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s",
+               h16 ? "gemm_h16_kernel" : (c->hnp == 3 && c->sw.gemm_h3) ? "gemm_h3_kernel" : "gemm_h_kernel",
                lay[AL], lay[BL], c->hnp, name);
       ProfScope ps(c, key, 2.0 * M * N * (double)K,
                    2.0 * c->hnp * ((double)M * K + (double)K * N) +
@@ -674,6 +681,9 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
         hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else if (c->hnp == 1)
         hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
+      else if (c->sw.gemm_h3)
+        // the same kernel with immediate-offset addressing (gemm_h3.h)
+        hipLaunchKernelGGL((gemm_h3_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
       else
         // SCH 1: fragment reads spread over the MFMA gaps (+2-4 % over the
         // burst schedule, bitwise equal; profiles/r3/gemmh_sched_c3.txt)
@@ -1874,7 +1884,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_s3 = !env_is("DDPG_GEMM", "f32");
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
-      if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = std::min(3, std::max(0, atoi(v)));
+      c->sw.gemm_h3 = !env_is("DDPG_GEMM_H3", "0");
+      if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = std::min(4, std::max(0, atoi(v)));
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");

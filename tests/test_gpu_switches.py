@@ -15,6 +15,9 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       instead of as one five-part thin_k launch
     DDPG_ACT32=1      fp32 copies of h1 / cat / cat2 written beside their planes
                       (the default reads the EluGrad operand from the planes)
+    DDPG_GEMM_H3=0    fp32-context twin GEMM on gemm_h_kernel (runtime ring-slot
+                      addressing) instead of gemm_h3_kernel (immediate offsets):
+                      same products, same order
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
     DDPG_GEMM=f32     every GEMM on the fp32-input MFMA kernel (no twins)
     DDPG_GEMM_H=0     no twins; large GEMMs on gemm_s3 (operands split while staging)
@@ -38,7 +41,7 @@ pytestmark = pytest.mark.gpu
 
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
-            "DDPG_ACT32", "DDPG_GEMM256")
+            "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3")
 
 
 @pytest.fixture(scope="module")
@@ -122,6 +125,7 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_SB_XCD", "0", "ip"),
     ("DDPG_L1BATCH", "0", "wide"),
     ("DDPG_ACT32", "1", "wide"),
+    ("DDPG_GEMM_H3", "0", "wide"),
 ])
 def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
@@ -183,7 +187,7 @@ def test_gemm256_switch_bf16(dd, O, monkeypatch):
 @pytest.mark.parametrize("switch,value,kernel,absent", [
     ("DDPG_GEMM", "f32", "gemm_f32_kernel", "gemm_h"),
     ("DDPG_GEMM_H", "0", "gemm_s3_kernel", "gemm_h"),
-    ("DDPG_THINK", "0", "gemm_h_kernel", "thin_k_kernel"),
+    ("DDPG_THINK", "0", "gemm_h3_kernel", "thin_k_kernel"),
     ("DDPG_SKINNY", "0", "gemm_f32_kernel", "skinny_wgrad_kernel"),
 ])
 def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent):
