@@ -238,7 +238,7 @@ struct ddpg_ctx {
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
-    bool gemm_h3 = true;   // DDPG_GEMM_H3=0: fp32 twin GEMM on gemm_h_kernel (runtime slot addressing)
+    bool gemm_h3 = true;   // DDPG_GEMM_H3=0: twin GEMMs with runtime slot addressing (gemm_h_kernel / gemm_h16_kernel)
     int gemm256 = 0;       // DDPG_GEMM256=1 / 4: bf16 split-K weight gradients on gemm_h256.h; 2, 3: more shapes
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
@@ -671,13 +671,18 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
       char key[112];
       snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s",
-               h16 ? "gemm_h16_kernel" : (c->hnp == 3 && c->sw.gemm_h3) ? "gemm_h3_kernel" : "gemm_h_kernel",
+               h16 ? (AL == L_RK && c->sw.gemm_h3 ? "gemm_h16i_kernel" : "gemm_h16_kernel")
+                   : (c->hnp == 3 && c->sw.gemm_h3) ? "gemm_h3_kernel" : "gemm_h_kernel",
                lay[AL], lay[BL], c->hnp, name);
       ProfScope ps(c, key, 2.0 * M * N * (double)K,
                    2.0 * c->hnp * ((double)M * K + (double)K * N) +
                        4.0 * (double)M * N * h.splits);
       const dim3 grid(h.nt(N), h.mt(M), h.splits);
-      if (h16)
+      if (h16 && AL == L_RK && c->sw.gemm_h3) {
+        // immediate-offset addressing (gemm_h3.h), RK A operands
+        if constexpr (AL == L_RK)
+          hipLaunchKernelGGL((gemm_h16i_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
+      } else if (h16)
         hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else if (c->hnp == 1)
         hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);

@@ -276,3 +276,220 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
 }
 
 }  // namespace ddpg
+
+namespace ddpg {
+
+// The bf16-configuration GEMM gemm_h16_kernel<AL, BL, 1, 256, 64> (SCH = 0)
+// with cheaper addressing.  Its loop carried 24 v_subrev + 26 v_add + 10
+// v_lshl_add_u64 per 32 MFMAs, and a v_mfma_f32_16x16x32_bf16 gap hides only
+// about two VALU issues.  Here the ring slot stays a runtime value (a loop
+// unrolled by the three slots, as gemm_h3_kernel, spilled at 16x16x32's
+// register count) but is applied once per tile: every fragment read is a
+// per-lane base + the slot's byte offset (one v_add per base and tile) + an
+// immediate offset, and the LDS-DMA goes through buffer_load ... lds with the
+// k-tile advance in the scalar soffset.  RK A operands (forward, dX).  Same
+// schedule and MFMA order: bitwise equal to gemm_h16_kernel
+// (DDPG_GEMM_H3=0 selects it).
+template <int AL, int BL>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_kernel(GemmHArgs g) {
+  static_assert(AL == L_RK, "RK A operand");
+  constexpr int NP = 1, BM = 256, BK = 64;
+  using C = HgCfg<BM, BK, NP>;
+  constexpr int TM = BM / 64;   // 32-row blocks per wave (epilogue layout)
+  constexpr int TA = BM / 32;   // 16-row A fragments per wave
+  constexpr int TB = 2;         // 16-column B fragments per wave
+  constexpr int KS = BK / 32;   // 2 32-deep steps per tile
+  static_assert(C::A_PW == 4 && C::B_PW == 2 && KS == 2, "tile shape");
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM_BYTES / 4];
+  char* const lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int bx, by;
+  xcd_tile(bx, by, g.xcd);
+  const int n0 = bx * HG_BN, m0 = by * BM, z = blockIdx.z;
+  const int kbeg = z * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+
+  f32x4 acc[TA][TB];
+#pragma unroll
+  for (int i = 0; i < TA; ++i)
+#pragma unroll
+    for (int j = 0; j < TB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, 0x7fffffff, 0x00020000);
+  unsigned oa[C::A_PW], ob[C::B_PW];
+#pragma unroll
+  for (int i = 0; i < C::A_PW; ++i)
+    oa[i] = (unsigned)((const char*)hg_src<AL, BM, BK, 16>(g.A, g.lda, g.M, m0, kbeg,
+                                                          wave * C::A_PW + i, lane) -
+                       (const char*)g.A);
+#pragma unroll
+  for (int i = 0; i < C::B_PW; ++i)
+    ob[i] = (unsigned)((const char*)hg_src<BL, HG_BN, BK, 16>(g.B, g.ldb, g.N, n0, kbeg,
+                                                             wave * C::B_PW + i, lane) -
+                       (const char*)g.B);
+  const unsigned stepA = 2u * BK;  // RK A
+  const unsigned stepB = 2u * (BL == L_RK ? BK : (unsigned)BK * g.ldb);
+  // stage layout as gemm_h16_kernel: [A image | B image] per slot
+  auto piece = [&](int t, int buf, int q) {
+    char* base = lds + buf * C::STAGE;
+    if (q < C::A_PW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          ra, (lds_void*)(base + (wave * C::A_PW + q) * 1024), 16, oa[q], t * stepA, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (lds_void*)(base + C::A_BYTES + (wave * C::B_PW + q - C::A_PW) * 1024), 16,
+          ob[q - C::A_PW], t * stepB, 0, 0);
+  };
+  auto stage = [&](int t, int buf) {
+#pragma unroll
+    for (int q = 0; q < C::G; ++q) piece(t, buf, q);
+  };
+
+  // per-lane bases in slot 0.  RK image rows of 128 B, chunk
+  // (4 ks + (lane >> 4)) ^ ((r >> 1) & 7); rb % 16 == 0 leaves the swizzle to
+  // lane & 15 -> one pattern per ks.  KR B image ([64][128], kr_swz): per
+  // 16-column fragment j and k-row half.
+  const unsigned lbase = (unsigned)(uintptr_t)(lds_char*)lds;
+  auto rk_pat = [&](int rb, int ks) {
+    const int r = rb + (lane & 15);
+    return (unsigned)(r * (2 * BK) + 16 * ((4 * ks + (lane >> 4)) ^ ((r >> 1) & 7)));
+  };
+  auto kr_pat = [&](int rb, int half) {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int col = rb + 4 * p;
+    const int ch = (col & 127) >> 3;
+    const int k = 8 * (lane >> 4) + q + 4 * half;  // ks = 0; ks = 1 adds 32 rows (8 KB)
+    return (unsigned)((col >> 7) * (BK * 256) + k * 256 + 16 * (ch ^ kr_swz(k)) + 8 * (p & 1));
+  };
+  constexpr int NBB = BL == L_RK ? 2 : 2 * TB;
+  unsigned abase[2], bbase[NBB];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) abase[ks] = lbase + rk_pat(wm * (BM / 2), ks);
+#pragma unroll
+  for (int x = 0; x < NBB; ++x)
+    bbase[x] = lbase + C::A_BYTES +
+               (BL == L_RK ? rk_pat(wn * 32, x) : kr_pat(wn * 32 + 16 * (x >> 1), x & 1));
+  // the fragments of k-step KSR from the slot at byte offset so
+  auto read = [&](unsigned so, auto ks_c, bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
+    constexpr int KSR = decltype(ks_c)::value;
+    if constexpr (BL == L_RK) {
+      const unsigned b = bbase[KSR] + so;
+      static_for<TB>([&](auto j_c) {
+        constexpr int J = decltype(j_c)::value;
+        bv[0][J] = b128_read_off<J * 16 * (2 * BK)>(b);
+      });
+    } else {
+      static_for<TB>([&](auto j_c) {
+        constexpr int J = decltype(j_c)::value;
+        constexpr int OFF = KSR * 32 * 256;
+        bv[0][J] = __builtin_shufflevector(tr_read_off<OFF>(bbase[2 * J] + so),
+                                           tr_read_off<OFF>(bbase[2 * J + 1] + so), 0, 1, 2, 3,
+                                           4, 5, 6, 7);
+      });
+    }
+    const unsigned a = abase[KSR] + so;
+    static_for<TA>([&](auto i_c) {
+      constexpr int I = decltype(i_c)::value;
+      av[0][I] = b128_read_off<I * 16 * (2 * BK)>(a);
+    });
+  };
+  auto mfma_all = [&](bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+  };
+
+  bf16x8 fa[2][NP][TA], fb[2][NP][TB];
+  constexpr int NM = TA * TB;
+  // gemm_h16_kernel's tile: STAGE3: stage tile t+3 after X_t into tile t's
+  // slot; NEXT: tile t+1 exists; G2: tile t+2 was staged (vmcnt(G) at X_t)
+  auto tile = [&](int t, auto stage_c, auto next_c, auto g2_c) {
+    constexpr bool STAGE3 = decltype(stage_c)::value;
+    constexpr bool NEXT = decltype(next_c)::value;
+    constexpr bool G2 = decltype(g2_c)::value;
+    const int slot = t % HG_STAGES;
+    const unsigned so = (unsigned)slot * C::STAGE;
+    static_for<KS>([&](auto ks_c) {
+      constexpr int ks = decltype(ks_c)::value;
+      constexpr int cs = ks & 1, ns = (ks + 1) & 1;
+      hg_wait16<NP, TA, TB>(fa[cs], fb[cs]);
+      if constexpr (ks + 1 < KS) {
+        read(so, std::integral_constant<int, ks + 1>{}, fa[ns], fb[ns]);
+      } else if constexpr (NEXT) {
+        if constexpr (G2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read((unsigned)((slot + 1) % HG_STAGES) * C::STAGE, std::integral_constant<int, 0>{},
+             fa[ns], fb[ns]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_all(fa[cs], fb[cs]);
+      if constexpr (ks + 1 == KS && STAGE3) {
+        stage(t + 3, slot);
+        constexpr int NG = C::G, MPG = NM / NG > 0 ? NM / NG : 1;
+        static_for<NG>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, MPG, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        });
+        if constexpr (NM - MPG * NG > 0)
+          __builtin_amdgcn_sched_group_barrier(0x008, NM - MPG * NG, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  if (nk > 0) {
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    if (nk > 2) {
+      stage(2, 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C::G) : "memory");
+    } else if (nk > 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(0u, std::integral_constant<int, 0>{}, fa[0], fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    int t = 0;
+    for (; t + 3 < nk; ++t) tile(t, T_{}, T_{}, T_{});  // stages t+3; t+2 in flight
+    if (t + 2 < nk) tile(t++, F_{}, T_{}, T_{});         // t+2 in flight
+    if (t + 1 < nk) tile(t++, F_{}, T_{}, F_{});
+    tile(t, F_{}, F_{}, F_{});
+  }
+  // repack into the 32x32 register layout of gemm_epilogue<..., 16>
+  f32x16 out[TM][1];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[i][0][4 * (2 * tr + tc) + q] = acc[2 * i + tr][tc][q];
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // staging buffers are reused by the epilogue
+  GemmArgs ge;
+  ge.M = g.M;
+  ge.N = g.N;
+  ge.e = g.e;
+  gemm_epilogue<BM, HG_BN, 4, 16>(out, smem, ge, tid, n0, m0, z, bx, by);
+}
+
+}  // namespace ddpg

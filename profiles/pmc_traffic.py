@@ -46,6 +46,8 @@ def bench_name(rocprof_name):
         return "%s<%s,%s,NP=%s>" % (sym, a[0], a[1], a[2])
     if sym == "gemm_h3_kernel" and len(a) == 2:  # three planes by construction
         return "%s<%s,%s,NP=3>" % (sym, a[0], a[1])
+    if sym == "gemm_h16i_kernel" and len(a) == 2:  # one plane by construction
+        return "%s<%s,%s,NP=1>" % (sym, a[0], a[1])
     if sym == "gemm_h256_kernel" and len(a) == 3:
         return "%s<%s,%s,MODE=%s>" % (sym, a[0], a[1], a[2])
     return "%s<%s>" % (sym, ",".join(a))

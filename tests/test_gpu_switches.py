@@ -15,9 +15,9 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       instead of as one five-part thin_k launch
     DDPG_ACT32=1      fp32 copies of h1 / cat / cat2 written beside their planes
                       (the default reads the EluGrad operand from the planes)
-    DDPG_GEMM_H3=0    fp32-context twin GEMM on gemm_h_kernel (runtime ring-slot
-                      addressing) instead of gemm_h3_kernel (immediate offsets):
-                      same products, same order
+    DDPG_GEMM_H3=0    twin GEMMs with runtime ring-slot addressing (gemm_h_kernel,
+                      gemm_h16_kernel) instead of gemm_h3_kernel / gemm_h16i_kernel
+                      (gemm_h3.h): same products, same order (fp32 and bf16)
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
     DDPG_GEMM=f32     every GEMM on the fp32-input MFMA kernel (no twins)
     DDPG_GEMM_H=0     no twins; large GEMMs on gemm_s3 (operands split while staging)
@@ -148,6 +148,22 @@ def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
     got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
     assert any(k.startswith("gemm_h_kernel") and "NP=1" in k for k in got["keys"]), got["keys"]
     assert not any(k.startswith("gemm_h16_kernel") for k in got["keys"]), got["keys"]
+    _bitwise(got, ref)
+
+
+def test_gemm_h3_switch_bf16_bitwise(dd, O, monkeypatch):
+    """bf16 configuration: the forward / dX GEMMs on gemm_h16i_kernel (per-tile
+    slot base + immediate offsets, gemm_h3.h) by default and on
+    gemm_h16_kernel with DDPG_GEMM_H3=0 -- same products in the same order,
+    bitwise equal results after 2 fused steps."""
+    _clear(monkeypatch)
+    p, _ = _params(O, "wide")
+    ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
+    assert any(k.startswith("gemm_h16i_kernel<RK,KR") for k in ref["keys"]), ref["keys"]
+    assert any(k.startswith("gemm_h16i_kernel<RK,RK") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_GEMM_H3", "0")
+    got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
+    assert not any(k.startswith("gemm_h16i_kernel") for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 
