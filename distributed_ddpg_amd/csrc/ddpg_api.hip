@@ -245,6 +245,7 @@ struct ddpg_ctx {
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
     bool l1_batch = true;  // DDPG_L1BATCH=0: the step's first layers per network
     bool act_planes = true;  // DDPG_ACT32=1: fp32 copies of h1 / cat / cat2 as well
+    int tk_rpb = 0;          // DDPG_TK_RPB=n: thin_k row tiles per block (0: auto)
   } sw;
 
   // comm: every collective of the ctx is issued on cs (one stream, so the
@@ -820,11 +821,24 @@ static int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int
   }
   a.M = M;
   const int mt = ceil_div(M, TK_ROWS);
+  const int nc = ceil_div(nmax, TK_COLS);
+  // row tiles per block: the fewest that keep the grid within one round of
+  // the chip's block slots (256 CUs x 2 blocks of 72 KB LDS), so that a block
+  // stages its W panel once for several row tiles and overlaps the next X
+  // tile's loads with its stores (env DDPG_TK_RPB=n forces n; 1 = one tile)
+  int rpb = 1;
+  if (c->sw.tk_rpb > 0) {
+    rpb = std::min(c->sw.tk_rpb, mt);
+  } else {
+    constexpr int kSlots = 256 * 2;
+    while (rpb < mt && nc * nparts * ceil_div(mt, rpb) > kSlots) ++rpb;
+  }
+  a.mt = mt;
+  a.rpb = rpb;
   char key[96];
   snprintf(key, sizeof key, "thin_k_kernel|%s", name);
   ProfScope ps(c, key, flops, bytes);
-  hipLaunchKernelGGL(thin_k_kernel, dim3(ceil_div(nmax, TK_COLS), mt, nparts), dim3(TK_NT), 0,
-                     c->cur, a);
+  hipLaunchKernelGGL(thin_k_kernel, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0, c->cur, a);
   HIP_TRY(hipGetLastError());
   return mt;
 }
@@ -1896,6 +1910,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
       c->sw.l1_batch = !env_is("DDPG_L1BATCH", "0");
       c->sw.act_planes = !env_is("DDPG_ACT32", "1");
+      if (const char* v = getenv("DDPG_TK_RPB")) c->sw.tk_rpb = std::max(0, atoi(v));
     }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;

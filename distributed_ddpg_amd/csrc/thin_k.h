@@ -65,49 +65,86 @@ constexpr int TK_MAXP = 5;  // parts per launch (blockIdx.z)
 struct TkArgs {
   TkPart p[TK_MAXP];
   int M;
+  int mt;   // row tiles (ceil(M / TK_ROWS))
+  int rpb;  // row tiles per block (blockIdx.y owns [rpb * y, rpb * y + rpb))
 };
 
-constexpr int TK_VLD = TK_COLS + 4;  // LDS row stride of the output tile (floats)
-
-// Three-plane bf16 images in LDS (the exact split x = h + m + l of every fp32
-// operand, as the twins of gemm_h.h): [plane][row][64 k] with 128-B rows,
-// 16-B chunk c of row r at c ^ ((r >> 1) & 7) -- every 32x32x16 fragment read
+// LDS: the W image (3 planes, resident for the whole block), then one region
+// shared by the X image (3 planes) of the current row tile and, after its
+// MFMAs, the raw output tile [64 rows][TK_COLS] (16-B chunks XOR-swizzled by
+// row: tk_oidx), then the column-sum scratch of the epilogue.
+constexpr int TK_XIMG = TK_ROWS * 128;  // bytes per X plane
+constexpr int TK_WIMG = TK_COLS * 128;  // bytes per W plane
+constexpr int TK_OUT_BYTES = TK_ROWS * TK_COLS * 4;
+constexpr int TK_XREG = 3 * TK_XIMG > TK_OUT_BYTES ? 3 * TK_XIMG : TK_OUT_BYTES;
+constexpr int TK_LDS = 3 * TK_WIMG + TK_XREG;
+static_assert(TK_LDS <= 80 * 1024, "two blocks per CU");
+static_assert(TK_RG * TK_COLS * 4 <= TK_XREG, "column-sum scratch aliases the output tile");
+// Three-plane bf16 images (the exact split x = h + m + l of every fp32
+// operand, as the twins of gemm_h.h): [plane][row][64 k] with 128-B rows, 16-B
+// chunk c of row r at c ^ ((r >> 1) & 7) -- every 32x32x16 fragment read
 // (lane: row l & 31, chunk 2 ks + (l >> 5)) is bank-conflict-free.  X rows are
 // batch rows; W rows are output columns (W^T), so both operands are read the
 // same way.
-constexpr int TK_XIMG = TK_ROWS * 128;  // bytes per X plane
-constexpr int TK_WIMG = TK_COLS * 128;  // bytes per W plane
-constexpr int TK_OUT_BYTES = TK_ROWS * TK_VLD * 4;
-constexpr int TK_WREG = 3 * TK_WIMG > TK_OUT_BYTES ? 3 * TK_WIMG : TK_OUT_BYTES;
-constexpr int TK_LDS = TK_WREG + 3 * TK_XIMG;
-static_assert(TK_RG * TK_COLS * 4 <= 3 * TK_XIMG, "column-sum scratch aliases the X image");
 DDPG_DEV int tk_swz(int r) { return (r >> 1) & 7; }
+// hipcc's waitcnt insertion treats an asm operand as a use: the wait for a
+// register's pending global load goes here instead of at its first real use
+// (where, behind branches and conditional stores, it becomes vmcnt(0) and
+// waits for every store issued since)
+#define TK_LANDED(x) asm volatile("" ::"v"(x))
 DDPG_DEV int tk_off(int r, int k) { return r * 128 + 16 * ((k >> 3) ^ tk_swz(r)) + 2 * (k & 7); }
+// output tile: float (r, n) -- the MFMA write of lanes h = 0 / 1 (rows r, r + 4)
+// lands in opposite 128-B halves of the banks
+DDPG_DEV int tk_oidx(int r, int n) {
+  return r * TK_COLS + (((n >> 2) ^ (((r >> 2) & 1) << 3)) << 2) + (n & 3);
+}
 
+// Block (column block x, row tiles [rpb y, rpb y + rpb), part z): the W panel
+// is loaded and split once; each row tile's X tile is loaded one tile ahead
+// (its global loads in flight under the current tile's MFMAs and epilogue
+// stores), so the stream of output stores -- what bounds these layers -- is
+// not interrupted by a fresh W-panel round trip per 64 rows.
 __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
-  // W image (3 planes), after the MFMAs the raw output tile [64 rows][TK_VLD];
-  // then the X image (3 planes)
   __shared__ __attribute__((aligned(16))) char lds[TK_LDS];
-  float* const Ws = reinterpret_cast<float*>(lds);
   char* const wimg = lds;
-  char* const ximg = lds + TK_WREG;
-  // column-sum scratch: the X image, dead after the MFMA phase
-  float* const red = reinterpret_cast<float*>(ximg);
+  char* const ximg = lds + 3 * TK_WIMG;
+  float* const Os = reinterpret_cast<float*>(ximg);   // output tile (after the MFMAs)
+  float* const red = reinterpret_cast<float*>(ximg);  // column-sum scratch (after the stores)
   const TkPart P = args.p[blockIdx.z];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, h = lane >> 5;
   const int wr = wave & 1, wc = wave >> 1;  // 32-row half, column half
-  const int m0 = blockIdx.y * TK_ROWS, n0 = blockIdx.x * TK_COLS;
-  if (n0 >= P.N) return;
+  const int n0 = blockIdx.x * TK_COLS;
+  const int rt0 = blockIdx.y * args.rpb, rt1 = min(args.mt, rt0 + args.rpb);
+  if (n0 >= P.N || rt0 >= rt1) return;
   TK_STAMP(0);
   const int K = P.K, M = args.M;
   const int KS = (K + 15) >> 4;  // 16-deep MFMA steps; k in [K, 16 KS) are zeros
   const int KP = 16 * KS;
-  // ---- global loads: thread (column c, k quads kq + 2 j) of the W panel, and
-  // 4 float4 quads of the X tile (64 rows x 16 quads)
+  // ---- X tile loads (64 rows x 16 quads, 4 float4 per thread)
+  f32x4 xg[4];
+  auto load_x = [&](int rt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15), m = rt * TK_ROWS + r;
+      xg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k < K && m < M) xg[j] = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + k);
+    }
+  };
+  load_x(rt0);
+  // ---- W panel: thread (column c, k quads kq + 2 j), split into its image once
   const int wcol = tid % TK_COLS, kq = tid / TK_COLS, wn = n0 + wcol;
-  f32x4 wv[TK_WJ], xg[4];
+  auto put4 = [&](char* img, int plane_bytes, int r, int k, f32x4 v) {
+    bf16x2 h0, m0_, l0, h1, m1, l1;
+    split3_pair(f32x2v{v[0], v[1]}, h0, m0_, l0);
+    split3_pair(f32x2v{v[2], v[3]}, h1, m1, l1);
+    const int off = tk_off(r, k);
+    *reinterpret_cast<bf16x4*>(img + off) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+    *reinterpret_cast<bf16x4*>(img + plane_bytes + off) = bf16x4{m0_[0], m0_[1], m1[0], m1[1]};
+    *reinterpret_cast<bf16x4*>(img + 2 * plane_bytes + off) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+  };
   {
+    f32x4 wv[TK_WJ];
     const bool wvec = P.w_nk && ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
 #pragma unroll
     for (int j = 0; j < TK_WJ; ++j) {
@@ -123,88 +160,13 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
         }
       }
     }
-  }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15), m = m0 + r;
-    xg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (k < K && m < M) xg[j] = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + k);
-  }
-  // ---- split into the plane images
-  auto put4 = [&](char* img, int plane_bytes, int r, int k, f32x4 v) {
-    bf16x2 h0, m0_, l0, h1, m1, l1;
-    split3_pair(f32x2v{v[0], v[1]}, h0, m0_, l0);
-    split3_pair(f32x2v{v[2], v[3]}, h1, m1, l1);
-    const int off = tk_off(r, k);
-    *reinterpret_cast<bf16x4*>(img + off) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
-    *reinterpret_cast<bf16x4*>(img + plane_bytes + off) = bf16x4{m0_[0], m0_[1], m1[0], m1[1]};
-    *reinterpret_cast<bf16x4*>(img + 2 * plane_bytes + off) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
-  };
-#pragma unroll
-  for (int j = 0; j < TK_WJ; ++j) {
-    const int k = 4 * (kq + TK_KQS * j);
-    if (k < KP) put4(wimg, TK_WIMG, wcol, k, wv[j]);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15);
-    if (k < KP) put4(ximg, TK_XIMG, r, k, xg[j]);
-  }
-  __syncthreads();
-  TK_STAMP(1);
-  // ---- MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulation): per 16-deep step
-  // the six plane products hh, hm, mh, hl, lh, mm of gemm_h.h, the five small
-  // ones in their own accumulator.  Wave (wr, wc): rows 32 wr + li, columns
-  // (TK_COLS / 2) wc + 32 t + li (t < TK_TPW).
-  f32x16 acc[TK_TPW], acs[TK_TPW];
-#pragma unroll
-  for (int t = 0; t < TK_TPW; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = acs[t][r] = 0.f;
-  const int ra = 32 * wr + li;
-  for (int ks = 0; ks < KS; ++ks) {
-    const int kk = 16 * ks + 8 * h;
-    bf16x8 a[3], b[TK_TPW][3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      a[p] = *reinterpret_cast<const bf16x8*>(ximg + p * TK_XIMG + tk_off(ra, kk));
-#pragma unroll
-      for (int t = 0; t < TK_TPW; ++t)
-        b[t][p] = *reinterpret_cast<const bf16x8*>(wimg + p * TK_WIMG +
-                                                   tk_off((TK_COLS / 2) * wc + 32 * t + li, kk));
-    }
-#pragma unroll
-    for (int t = 0; t < TK_TPW; ++t) {
-      f32x16 q = acs[t];
-      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[t][0], q, 0, 0, 0);
-      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][1], q, 0, 0, 0);
-      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][2], q, 0, 0, 0);
-      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][0], q, 0, 0, 0);
-      q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][1], q, 0, 0, 0);
-      acs[t] = q;
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][0], acc[t], 0, 0, 0);
+    for (int j = 0; j < TK_WJ; ++j) {
+      const int k = 4 * (kq + TK_KQS * j);
+      if (k < KP) put4(wimg, TK_WIMG, wcol, k, wv[j]);
     }
   }
-#pragma unroll
-  for (int t = 0; t < TK_TPW; ++t) acc[t] += acs[t];
-  TK_STAMP(2);
-  // ---- epilogue.  The raw tile goes through LDS (lane li of tile t holds
-  // column li, register r row (r & 3) + 8 (r >> 2) + 4 h) so that every
-  // element-wise op, the aux loads and the output stores run on float4 rows:
-  // one 16-B access per lane instead of 32 scalar 4-B stores per lane.
-  __syncthreads();  // all waves done reading the W panel
-  {
-    const int rb = 32 * wr + 4 * h;
-#pragma unroll
-    for (int t = 0; t < TK_TPW; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        Ws[(rb + (r & 3) + 8 * (r >> 2)) * TK_VLD + (TK_COLS / 2) * wc + 32 * t + li] = acc[t][r];
-  }
-  __syncthreads();
-  TK_STAMP(3);
-  // thread -> column octet c8 = tid & 15, rows rg + 16 i (rg = tid >> 4):
-  // 16-B fp32 and twin-plane stores
+  // per-thread epilogue constants: column octet c8, rows rg + TK_RG i
   const int c8 = tid % TK_OCT, rg = tid / TK_OCT, n = n0 + 8 * c8;
   const bool q0 = n < P.N, q1 = n + 4 < P.N;  // N % 4 == 0: quads all in or all out
   const bool oct = q1 && ((P.ldo & 7) == 0) && ((P.hps & 7) == 0) &&
@@ -212,66 +174,145 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   f32x4 bq0 = f32x4{0.f, 0.f, 0.f, 0.f}, bq1 = bq0;
   if (P.bias && q0) bq0 = *reinterpret_cast<const f32x4*>(P.bias + n);
   if (P.bias && q1) bq1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
-  float csum[8];
+  const int ra = 32 * wr + li;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-  constexpr int RPT = TK_ROWS / TK_RG;  // rows per thread
-  f32x4 aq[RPT][2];
-  if (P.aux) {  // all aux loads in flight before the first use
+  for (int j = 0; j < 4; ++j) TK_LANDED(xg[j]);
+  TK_LANDED(bq0);
+  TK_LANDED(bq1);
+
+  for (int rt = rt0; rt < rt1; ++rt) {
+    const int m0 = rt * TK_ROWS;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15);
+      if (k < KP) put4(ximg, TK_XIMG, r, k, xg[j]);
+    }
+    __syncthreads();  // X image (and, first trip, the W image) complete
+    TK_STAMP(1);
+    if (rt + 1 < rt1) load_x(rt + 1);  // next tile's loads in flight from here
+    // ---- MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulation): per 16-deep
+    // step the six plane products hh, hm, mh, hl, lh, mm of gemm_h.h, the five
+    // small ones in their own accumulator.  Wave (wr, wc): rows 32 wr + li,
+    // columns (TK_COLS / 2) wc + 32 t + li (t < TK_TPW).
+    f32x16 acc[TK_TPW], acs[TK_TPW];
+#pragma unroll
+    for (int t = 0; t < TK_TPW; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = acs[t][r] = 0.f;
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kk = 16 * ks + 8 * h;
+      bf16x8 a[3], b[TK_TPW][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a[p] = *reinterpret_cast<const bf16x8*>(ximg + p * TK_XIMG + tk_off(ra, kk));
+#pragma unroll
+        for (int t = 0; t < TK_TPW; ++t)
+          b[t][p] = *reinterpret_cast<const bf16x8*>(
+              wimg + p * TK_WIMG + tk_off((TK_COLS / 2) * wc + 32 * t + li, kk));
+      }
+#pragma unroll
+      for (int t = 0; t < TK_TPW; ++t) {
+        f32x16 q = acs[t];
+        q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[t][0], q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][1], q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][2], q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][0], q, 0, 0, 0);
+        q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][1], q, 0, 0, 0);
+        acs[t] = q;
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][0], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TK_TPW; ++t) acc[t] += acs[t];
+    TK_STAMP(2);
+    // ---- epilogue.  The raw tile goes through LDS (lane li of tile t holds
+    // column li, register r row (r & 3) + 8 (r >> 2) + 4 h) so that every
+    // element-wise op, the aux loads and the output stores run on float4 rows.
+    __syncthreads();  // every wave done reading the X image
+    {
+      const int rb = 32 * wr + 4 * h;
+#pragma unroll
+      for (int t = 0; t < TK_TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Os[tk_oidx(rb + (r & 3) + 8 * (r >> 2), (TK_COLS / 2) * wc + 32 * t + li)] = acc[t][r];
+    }
+    __syncthreads();
+    TK_STAMP(3);
+    float csum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+    constexpr int RPT = TK_ROWS / TK_RG;  // rows per thread
+    f32x4 aq[RPT][2];
+    if (P.aux) {  // all aux loads in flight before the first use
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int m = m0 + rg + TK_RG * i;
+        aq[i][0] = aq[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m < M) {
+          const float* ap = P.aux + (size_t)m * P.ldaux + n;
+          if (q0) aq[i][0] = *reinterpret_cast<const f32x4*>(ap);
+          if (q1) aq[i][1] = *reinterpret_cast<const f32x4*>(ap + 4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        TK_LANDED(aq[i][0]);
+        TK_LANDED(aq[i][1]);
+      }
+    }
+    // every load this tile's stores could be ordered behind (the aux rows
+    // above, the next X tile) has landed here, before the first store: the
+    // row loop below then carries no vmcnt wait, and the next trip's put4 of
+    // xg none either -- the stores stream while the next tile's MFMAs run
+#pragma unroll
+    for (int j = 0; j < 4; ++j) TK_LANDED(xg[j]);
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const int m = m0 + rg + TK_RG * i;
-      aq[i][0] = aq[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (m < M) {
-        const float* ap = P.aux + (size_t)m * P.ldaux + n;
-        if (q0) aq[i][0] = *reinterpret_cast<const f32x4*>(ap);
-        if (q1) aq[i][1] = *reinterpret_cast<const f32x4*>(ap + 4);
+      const int rl = rg + TK_RG * i, m = m0 + rl;
+      if (!q0 || m >= M) continue;
+      f32x4 v[2];
+      v[0] = *reinterpret_cast<const f32x4*>(Os + tk_oidx(rl, 8 * c8));
+      v[1] = *reinterpret_cast<const f32x4*>(Os + tk_oidx(rl, 8 * c8 + 4));
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = v[u][e];
+          if (P.bias) x = __fadd_rn(x, u ? bq1[e] : bq0[e]);
+          if (P.act == 1) x = elu_f(x);
+          if (P.aux) x = __fmul_rn(x, elu_grad_factor(aq[i][u][e]));
+          v[u][e] = x;
+          if (u == 0 || q1) csum[4 * u + e] += x;
+        }
+      const size_t o = (size_t)m * P.ldo + n;
+      const float4 va = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]);
+      const float4 vb = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
+      if (P.out) {
+        *reinterpret_cast<f32x4*>(P.out + o) = v[0];
+        if (q1) *reinterpret_cast<f32x4*>(P.out + o + 4) = v[1];
+      }
+      if (P.outh) {
+        if (oct) {
+          store_twin8(P.outh + o, P.hps, P.hnp, va, vb);
+        } else {
+          store_twin4(P.outh + o, P.hps, P.hnp, va);
+          if (q1) store_twin4(P.outh + o + 4, P.hps, P.hnp, vb);
+        }
       }
     }
-  }
+    __syncthreads();  // output tile read: the region is next the column-sum scratch / X image
+    if (P.colsum) {
 #pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int rl = rg + TK_RG * i, m = m0 + rl;
-    if (!q0 || m >= M) continue;
-    f32x4 v[2];
-    v[0] = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 8 * c8);
-    v[1] = *reinterpret_cast<const f32x4*>(Ws + rl * TK_VLD + 8 * c8 + 4);
+      for (int e = 0; e < 8; ++e) red[rg * TK_COLS + 8 * c8 + e] = csum[e];
+      __syncthreads();
+      if (tid < TK_COLS && n0 + tid < P.N) {
+        float s = 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = v[u][e];
-        if (P.bias) x = __fadd_rn(x, u ? bq1[e] : bq0[e]);
-        if (P.act == 1) x = elu_f(x);
-        if (P.aux) x = __fmul_rn(x, elu_grad_factor(aq[i][u][e]));
-        v[u][e] = x;
-        if (u == 0 || q1) csum[4 * u + e] += x;
+        for (int g = 0; g < TK_RG; ++g) s += red[g * TK_COLS + tid];
+        P.colsum[(size_t)rt * P.ld_colsum + n0 + tid] = s;
       }
-    const size_t o = (size_t)m * P.ldo + n;
-    const float4 va = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]);
-    const float4 vb = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
-    if (P.out) {
-      *reinterpret_cast<f32x4*>(P.out + o) = v[0];
-      if (q1) *reinterpret_cast<f32x4*>(P.out + o + 4) = v[1];
-    }
-    if (P.outh) {
-      if (oct) {
-        store_twin8(P.outh + o, P.hps, P.hnp, va, vb);
-      } else {
-        store_twin4(P.outh + o, P.hps, P.hnp, va);
-        if (q1) store_twin4(P.outh + o + 4, P.hps, P.hnp, vb);
-      }
-    }
-  }
-  if (P.colsum) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[rg * TK_COLS + 8 * c8 + e] = csum[e];
-    __syncthreads();
-    if (tid < TK_COLS && n0 + tid < P.N) {
-      float s = 0.f;
-#pragma unroll
-      for (int g = 0; g < TK_RG; ++g) s += red[g * TK_COLS + tid];
-      P.colsum[(size_t)blockIdx.y * P.ld_colsum + n0 + tid] = s;
+      __syncthreads();
     }
   }
 }

@@ -58,8 +58,11 @@ static float time_it(const TkArgs& a, int nparts, int reps) {
 
 static void run_all();
 int main() {
-  printf("== new thin_k_kernel\n");
+  printf("== thin_k_kernel, one row tile per block\n");
   g_rb = 4096 / TK_ROWS;
+  run_all();
+  printf("== thin_k_kernel, 4 row tiles per block\n");
+  g_rb = 4096 / TK_ROWS / 4;
   run_all();
 #ifdef WITH_OLD
   printf("== old thin_k_kernel\n");
@@ -90,6 +93,8 @@ static void run_all() {
   TkArgs a;
   memset(&a, 0, sizeof a);
   a.M = M;
+  a.mt = M / TK_ROWS;
+  a.rpb = (a.mt + g_rb - 1) / g_rb;  // row tiles per block for g_rb row blocks
   a.p[0] = p;
   printf("K64 bias+elu+store           %.2f us\n", time_it(a, 1, 200));
   phases("K64", 8 * g_rb);
