@@ -447,8 +447,10 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceTable tab) {
 //   alpha = lr * sqrt(1 - b2p) / (1 - b1p)
 //   m += (g - m) * (1 - b1);  v += (g*g - v) * (1 - b2)
 //   p -= (m * alpha) / (sqrt(v) + eps)
-// The beta powers live on device (pw = {b1p, b2p}); the last block to finish
-// advances them (b1p *= b1, b2p *= b2), i.e. the AdamOptimizer._finish update.
+// The beta powers live on device (pw = {b1p, b2p}); advance_powers_kernel,
+// launched after the pass, advances them (b1p *= b1, b2p *= b2), i.e. the
+// AdamOptimizer._finish update (folding it into this kernel's last-arriving
+// block was slower: profiles/r3/adam_adv_fold_ab.txt).
 // tw (optional): the bf16 twin of p (tnp planes, tps elements apart), kept
 // current for the bf16-operand GEMMs.
 // tt (optional, fused learner step): the network's target parameters, soft-

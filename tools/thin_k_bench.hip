@@ -64,6 +64,9 @@ int main() {
   printf("== thin_k_kernel, 4 row tiles per block\n");
   g_rb = 4096 / TK_ROWS / 4;
   run_all();
+  printf("== thin_k_kernel, 6 row tiles per block\n");
+  g_rb = (4096 / TK_ROWS + 5) / 6;
+  run_all();
 #ifdef WITH_OLD
   printf("== old thin_k_kernel\n");
   g_kern = old::thin_k_old_kernel;
@@ -126,6 +129,37 @@ static void run_all() {
   a.p[1].out = out + N;
   a.p[1].K = 16; a.p[1].ldx = 16;
   printf("2 parts K64|K16              %.2f us\n", time_it(a, 2, 200));
+  {  // the large-batch step's five-part first-layer launch: 3-plane twins only
+    __bf16* tw;
+    const size_t ne = (size_t)M * N;
+    hipMalloc(&tw, ne * 2 * 3 * 5);
+    TkPart f = p;
+    f.out = nullptr;
+    f.ldo = N;
+    f.hnp = 3;
+    f.hps = (long long)ne * 5;
+    for (int i = 0; i < 5; ++i) {
+      a.p[i] = f;
+      a.p[i].outh = tw + ne * i;
+      if (i == 4) { a.p[i].K = 16; a.p[i].ldx = 16; }
+    }
+    printf("5 parts twin-only K64x4|K16  %.2f us\n", time_it(a, 5, 100));
+    phases("5 parts", 8 * g_rb * 5);
+    for (int i = 0; i < 5; ++i) a.p[i].outh = nullptr;
+    printf("5 parts no store             %.2f us\n", time_it(a, 5, 100));
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0);
+    for (int i = 0; i < 50; ++i) hipMemsetAsync(tw, 0, ne * 2 * 3 * 5);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("hipMemset 126 MB             %.2f us\n", 1e3f * ms / 50);
+    hipFree(tw);
+    memset(&a.p, 0, sizeof a.p);
+  }
   // dz2: K = 16, w_nk, aux, colsum, no bias / act
   TkPart q = p;
   q.K = 16; q.ldx = 16; q.w_nk = 1; q.ldw = 16; q.bias = nullptr; q.act = 0;
