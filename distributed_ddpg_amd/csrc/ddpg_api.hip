@@ -195,6 +195,10 @@ struct ddpg_ctx {
   size_t act_n = 0;
   std::vector<std::pair<const float*, size_t>> twinned;
   int split_cap_W1, split_cap_W2, split_cap_W3, split_cap_Ws, split_cap_Wa, split_cap_Wh;
+  // the step's replay slots as the gather / phase kernels read them: the
+  // pinned host buffer the sampler filled (device-readable; no upload), or
+  // d_slots after a hipMemcpyAsync with DDPG_SLOTS_H2D=1
+  const int* slots_src = nullptr;
   int* d_slots = nullptr;
   int* h_slots = nullptr;  // pinned, kSlotRing x Bmax
   hipEvent_t slot_ev[4];
@@ -245,6 +249,7 @@ struct ddpg_ctx {
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
     bool l1_batch = true;  // DDPG_L1BATCH=0: the step's first layers per network
     bool act_planes = true;  // DDPG_ACT32=1: fp32 copies of h1 / cat / cat2 as well
+    bool slots_h2d = false;  // DDPG_SLOTS_H2D=1: upload the step's slots instead of reading them in place
     int tk_rpb = 0;          // DDPG_TK_RPB=n: thin_k row tiles per block (0: auto)
   } sw;
 
@@ -1625,7 +1630,7 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   a.lr_a = c->cfg.actor_lr;
   a.lr_c = c->cfg.critic_lr;
   a.eps = c->cfg.epsilon;
-  a.slots = c->d_slots;
+  a.slots = c->slots_src ? c->slots_src : c->d_slots;
   if (rb) {
     a.rs = rb->rs;
     a.ra = rb->ra;
@@ -1910,6 +1915,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
       c->sw.l1_batch = !env_is("DDPG_L1BATCH", "0");
       c->sw.act_planes = !env_is("DDPG_ACT32", "1");
+      c->sw.slots_h2d = env_is("DDPG_SLOTS_H2D", "1");
       if (const char* v = getenv("DDPG_TK_RPB")) c->sw.tk_rpb = std::max(0, atoi(v));
     }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
@@ -2699,7 +2705,8 @@ int ddpg_replay_sample_batch_f64(ddpg_replay* rb, int B, double* s, float* a, do
 static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
   ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
   hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->cur,
-                     c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt, rb->rs2, rb->rsd, rb->rs2d,
+                     c->slots_src ? c->slots_src : c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt,
+                     rb->rs2, rb->rsd, rb->rs2d,
                      rb->rrd, c->S, c->A, c->s,
                      c->s2, c->ldS, c->a, c->ldA, c->r, c->t, c->has_scaler ? c->dmean : nullptr,
                      c->has_scaler ? c->dscale : nullptr, act_twin(c, c->s).p,
@@ -2734,10 +2741,18 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
       hipGraph_t graph;
       HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
       try {
-        HIP_TRY(hipMemcpyAsync(c->d_slots, g.h_idx, (size_t)B * sizeof(int),
-                               hipMemcpyHostToDevice, c->stream));
+        if (c->sw.slots_h2d) {
+          HIP_TRY(hipMemcpyAsync(c->d_slots, g.h_idx, (size_t)B * sizeof(int),
+                                 hipMemcpyHostToDevice, c->stream));
+          c->slots_src = c->d_slots;
+        } else {
+          c->slots_src = g.h_idx;  // read in place by the replay (pinned; rewritten only
+                                   // after this slot's previous replay is done)
+        }
         learner_step_any(c, rb, B, inv_b);
+        c->slots_src = nullptr;
       } catch (...) {
+        c->slots_src = nullptr;
         (void)hipStreamEndCapture(c->stream, &graph);
         throw;
       }
@@ -2756,10 +2771,21 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     HIP_TRY(hipEventSynchronize(c->slot_ev[si]));
     int* hs = c->h_slots + (size_t)si * c->Bmax;
     for (int i = 0; i < B; ++i) hs[i] = pos_to_slot(rb, mine[i]);
-    HIP_TRY(hipMemcpyAsync(c->d_slots, hs, (size_t)B * sizeof(int), hipMemcpyHostToDevice,
-                           c->stream));
+    if (c->sw.slots_h2d) {
+      HIP_TRY(hipMemcpyAsync(c->d_slots, hs, (size_t)B * sizeof(int), hipMemcpyHostToDevice,
+                             c->stream));
+      c->slots_src = c->d_slots;
+    } else {
+      c->slots_src = hs;  // read in place (pinned; reused kSlotRing steps later, after slot_ev)
+    }
+    try {
+      learner_step_any(c, rb, B, inv_b);
+    } catch (...) {
+      c->slots_src = nullptr;
+      throw;
+    }
+    c->slots_src = nullptr;
     HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
-    learner_step_any(c, rb, B, inv_b);
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
   // Host-side state flags, updated here because a graph replay runs no host

@@ -20,6 +20,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       (gemm_h3.h): same products, same order (fp32 and bf16)
     DDPG_TK_RPB=3     thin_k blocks walk 3 row tiles each (W panel staged once,
                       next X tile prefetched) instead of the automatic count
+    DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
+                      instead of read in place from the pinned host buffer
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
     DDPG_GEMM=f32     every GEMM on the fp32-input MFMA kernel (no twins)
     DDPG_GEMM_H=0     no twins; large GEMMs on gemm_s3 (operands split while staging)
@@ -43,7 +45,8 @@ pytestmark = pytest.mark.gpu
 
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
-            "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB")
+            "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
+            "DDPG_SLOTS_H2D")
 
 
 @pytest.fixture(scope="module")
@@ -129,6 +132,8 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_ACT32", "1", "wide"),
     ("DDPG_GEMM_H3", "0", "wide"),
     ("DDPG_TK_RPB", "3", "wide"),
+    ("DDPG_SLOTS_H2D", "1", "wide"),
+    ("DDPG_SLOTS_H2D", "1", "ip"),
 ])
 def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
