@@ -216,6 +216,17 @@ struct ddpg_ctx {
     hipEvent_t done = nullptr;
   } gslot[2];
   int gcur = 0;
+  // issue policy of the small-batch path (DDPG_GRAPH_AUTO=0: always the
+  // graph): a step that finds the previous one finished (a caller that
+  // synchronises every step, as the reference's worker does) replays the
+  // graph -- the lower latency; a step issued while the previous is still
+  // running (a pipelined caller) is launched eagerly -- the higher throughput
+  // (its 4 launches stream back to back, where a graph launch stalls the queue
+  // at its boundary: C2 +4 % same box; at large B the two measured equal, so
+  // the large path always replays).  Both issue the same kernels in the same
+  // order (bitwise equal results).
+  bool graph_auto = true;
+  hipEvent_t step_done = nullptr;
   bool use_graph = true;
   bool par = false;  // env DDPG_PAR=1: fork independent branches onto aux streams
   // small-batch fused path (small_batch.h): eligible dims, per-WG gradient slabs
@@ -1784,6 +1795,7 @@ static void ctx_free(ddpg_ctx* c) {
     if (g.h_idx) (void)hipHostFree(g.h_idx);
     if (g.done) (void)hipEventDestroy(g.done);
   }
+  if (c->step_done) (void)hipEventDestroy(c->step_done);
   for (void* p : {(void*)c->sb_save, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T,
                   (void*)c->sb_stamps})
     if (p) (void)hipFree(p);
@@ -2003,7 +2015,9 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       HIP_TRY(hipHostMalloc(&g.h_idx, B * sizeof(int)));
       HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
     }
+    HIP_TRY(hipEventCreateWithFlags(&c->step_done, hipEventDisableTiming));
     if (const char* gv = getenv("DDPG_GRAPH")) c->use_graph = atoi(gv) != 0;
+    if (const char* gv = getenv("DDPG_GRAPH_AUTO")) c->graph_auto = atoi(gv) != 0;
     if (const char* pv = getenv("DDPG_PAR")) c->par = atoi(pv) != 0;
     {
       const int hmax = std::max(std::max(c->AH1, c->AH2), std::max(c->CH1, c->CH2));
@@ -2730,7 +2744,13 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   // large-batch call (every 1:1 method and large step calls twins_refresh)
   if (!small) twins_refresh(c);
   // graphs: single-rank, not profiling (RCCL capture and per-kernel events stay eager)
-  if (c->use_graph && c->world == 1 && !c->comm && !c->prof) {
+  bool idle = true;  // the previous step has finished (never-recorded event: success)
+  if (c->graph_auto && small) {
+    const hipError_t q = hipEventQuery(c->step_done);
+    if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+    idle = q == hipSuccess;
+  }
+  if (c->use_graph && idle && c->world == 1 && !c->comm && !c->prof) {
     auto& g = c->gslot[c->gcur];
     c->gcur ^= 1;
     HIP_TRY(hipEventSynchronize(g.done));  // this slot's previous replay has finished
@@ -2788,6 +2808,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
+  HIP_TRY(hipEventRecord(c->step_done, c->stream));
   // Host-side state flags, updated here because a graph replay runs no host
   // code: a large-path step moved theta without refreshing the small path's
   // W^T shadows; a small-path step moved theta / target without their twins.

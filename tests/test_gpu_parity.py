@@ -363,31 +363,38 @@ def test_batch_4096_wide_step_properties(dd, O):
     sess.close()
 
 
-def test_graph_replay_matches_eager(dd, O, monkeypatch):
+@pytest.mark.parametrize("name", ["ip", "wide"])
+def test_graph_replay_matches_eager(dd, O, monkeypatch, name):
     """The hipGraph-replayed fused step is bit-identical to eager launches
-    (all kernels are deterministic: no atomics in any reduction)."""
+    (all kernels are deterministic: no atomics in any reduction).  Variants:
+    the default issue policy (graph replay when the previous step has
+    finished, eager launches when it is still running: steps without stats
+    are not synchronised, so this run mixes both), graph replay only
+    (DDPG_GRAPH_AUTO=0) and eager only (DDPG_GRAPH=0)."""
     from distributed_ddpg_amd import _lib
     from distributed_ddpg_amd.learner import FusedLearner
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
-    S, A, H1, H2, scale, B, _ = CONFIGS["ip"]
-    p, _ = _params(O, "ip")
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
     out = []
-    for graph in ("1", "0"):
+    for graph, auto in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("DDPG_GRAPH", graph)
-        sess, actor, critic = _session(dd, O, "ip", p)
+        monkeypatch.setenv("DDPG_GRAPH_AUTO", auto)
+        sess, actor, critic = _session(dd, O, name, p)
         rb = ReplayBuffer(2000, 99)
         _fill(rb, S, A, 1500, scale, seed=4)
         fl = FusedLearner(sess, rb, B)
-        stats = [fl.step(stats=(i % 2 == 0)) for i in range(5)]
+        stats = [fl.step(stats=(i % 3 == 0)) for i in range(7)]
         out.append((stats, [sess.get_params(w) for w in (_lib.ACTOR, _lib.CRITIC,
                                                          _lib.ACTOR_TARGET, _lib.CRITIC_TARGET)],
                     sess.get_adam_powers(0), sess.get_adam_powers(1)))
         sess.close()
-    (s1, p1, a1, c1), (s0, p0, a0, c0) = out
-    assert s1 == s0 and a1 == a0 and c1 == c0
-    for x, y in zip(p1, p0):
-        for u, v in zip(x, y):
-            assert np.array_equal(u, v)
+    s0, p0, a0, c0 = out[-1]
+    for s1, p1, a1, c1 in out[:-1]:
+        assert s1 == s0 and a1 == a0 and c1 == c0
+        for x, y in zip(p1, p0):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)
 
 
 # ---------------------------------------------------------------------- bf16

@@ -46,7 +46,7 @@ pytestmark = pytest.mark.gpu
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
-            "DDPG_SLOTS_H2D")
+            "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO")
 
 
 @pytest.fixture(scope="module")
