@@ -144,22 +144,35 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     *reinterpret_cast<bf16x4*>(img + 2 * plane_bytes + off) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
   };
   {
+    // every load unconditional (clamped into the panel, masked after): behind
+    // per-load branches hipcc put a vmcnt(0) before each group, one round
+    // trip per k quad
     f32x4 wv[TK_WJ];
     const bool wvec = P.w_nk && ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
+    const int wnc = min(wn, P.N - 1);
+    if (wvec) {  // W[n][k], 16-B rows: 4 consecutive k per load
 #pragma unroll
-    for (int j = 0; j < TK_WJ; ++j) {
-      const int k = 4 * (kq + TK_KQS * j);
-      wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (k < K && wn < P.N) {
-        if (P.w_nk) {  // W[n][k]: 4 consecutive k (rows of an unaligned stride as scalars)
-          const float* q = P.W + (size_t)wn * P.ldw + k;
-          wv[j] = wvec ? *reinterpret_cast<const f32x4*>(q) : f32x4{q[0], q[1], q[2], q[3]};
-        } else {  // W[k][n]: 4 rows of column n (each load coalesced over the 128 columns)
+      for (int j = 0; j < TK_WJ; ++j) {
+        const int k = 4 * (kq + TK_KQS * j);
+        wv[j] = *reinterpret_cast<const f32x4*>(P.W + (size_t)wnc * P.ldw + min(k, K - 4));
+      }
+    } else if (P.w_nk) {  // W[n][k] of an unaligned stride: scalars
 #pragma unroll
-          for (int e = 0; e < 4; ++e) wv[j][e] = P.W[(size_t)(k + e) * P.ldw + wn];
-        }
+      for (int j = 0; j < TK_WJ; ++j) {
+        const float* q = P.W + (size_t)wnc * P.ldw + min(4 * (kq + TK_KQS * j), K - 4);
+        wv[j] = f32x4{q[0], q[1], q[2], q[3]};
+      }
+    } else {  // W[k][n]: 4 rows of column n (each load coalesced over the 128 columns)
+#pragma unroll
+      for (int j = 0; j < TK_WJ; ++j) {
+        const int k = min(4 * (kq + TK_KQS * j), K - 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wv[j][e] = P.W[(size_t)(k + e) * P.ldw + wnc];
       }
     }
+#pragma unroll
+    for (int j = 0; j < TK_WJ; ++j)
+      if (4 * (kq + TK_KQS * j) >= K || wn >= P.N) wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < TK_WJ; ++j) {
       const int k = 4 * (kq + TK_KQS * j);
