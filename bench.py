@@ -110,8 +110,11 @@ def spawn_ranks(n):
 
 
 def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="fp32",
-                  per_gpu_b=None):
-    from distributed_ddpg_amd import networks as nets
+                  per_gpu_b=None, rb=None, proxy=False):
+    """Session + replay ring (filled, or `rb` reused) + fused learner.
+    proxy: world > 1 on ONE GPU -- rank `rank`'s share of a world-rank step
+    with a 1-rank stand-in communicator (ddpg_comm_init_proxy)."""
+    from distributed_ddpg_amd import _lib, networks as nets
     from distributed_ddpg_amd.learner import FusedLearner, fill_synthetic, init_comm
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
     S, A, H1, H2, B, scale, _ = CONFIGS[cfg_name]
@@ -126,13 +129,116 @@ def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="
     sess.run(nets.global_variables_initializer(seed=seed))   # same init on every rank
     actor.update_target_network()                            # ddpg.py:228-229
     critic.update_target_network()
-    init_comm(sess, rank, world)
-    rb = ReplayBuffer(replay_rows, seed, device=device)
-    t0 = time.time()
-    fill_synthetic(rb, S, A, replay_rows, scale=scale, seed=seed)   # identical on every rank
-    log("[bench] rank %d replay filled with %d rows in %.1fs" % (rank, replay_rows,
-                                                                 time.time() - t0))
+    if proxy:
+        _lib.check(_lib.lib.ddpg_comm_init_proxy(sess.ctx), sess.ctx)
+    else:
+        init_comm(sess, rank, world)
+    if rb is None:
+        rb = ReplayBuffer(replay_rows, seed, device=device)
+        t0 = time.time()
+        fill_synthetic(rb, S, A, replay_rows, scale=scale, seed=seed)   # identical on every rank
+        log("[bench] rank %d replay filled with %d rows in %.1fs" % (rank, replay_rows,
+                                                                     time.time() - t0))
     return sess, rb, FusedLearner(sess, rb, B * world), actor
+
+
+# ---------------------------------------------------------------- projected scaling
+# Exchange model for the N-GPU projection.  Stated inputs, not
+# measurements: xGMI links of ~153 GB/s bidirectional, taken as 64 GB/s
+# effective per direction; a ring all-reduce over N GPUs of one node uses the
+# N-1 direct links of each GPU, at RCCL_EFF of their sum (bus bandwidth); a
+# fixed latency per collective call.
+XGMI_LINK_GBS = 64.0
+RCCL_EFF = 0.7
+RCCL_LAT_US = {2: 12.0, 4: 16.0, 8: 24.0}
+
+
+def allreduce_us(nbytes, n, eff=RCCL_EFF):
+    """Modelled ring all-reduce time of nbytes over n GPUs: latency +
+    2(n-1)/n x bytes / bus bandwidth."""
+    if n <= 1 or nbytes <= 0:
+        return 0.0
+    busbw = (n - 1) * XGMI_LINK_GBS * eff      # GB/s
+    return RCCL_LAT_US[n] + 2.0 * (n - 1) / n * nbytes / (busbw * 1e3)
+
+
+def exchange_bytes(S, A, H1, H2):
+    """Bytes of each RCCL call of one data-parallel step (the ctx's flat
+    layout: critic dWh, the critic's other tensors + stats, actor dW2, the
+    actor's other tensors), fp32."""
+    ap = S * H1 + H1 + H1 * H2 + H2 + H2 * A
+    cp = S * H1 + H1 + A * H1 + H1 + 2 * H1 * H2 + H2 + H2 + 1
+    return {"critic_dWh": 4 * 2 * H1 * H2, "critic_rest": 4 * (cp - 2 * H1 * H2) + 8,
+            "actor_dW2": 4 * H1 * H2, "actor_rest": 4 * (ap - H1 * H2)}
+
+
+def exposed_exchange_us(xb, win_c_us, win_a_us, n, eff=RCCL_EFF):
+    """Exchange time on the critical path of one step: the dWh / dW2
+    all-reduces overlap the measured windows (the compute issued between the
+    exchange and the join), the tail calls are fully exposed."""
+    t = max(0.0, allreduce_us(xb["critic_dWh"], n, eff) - win_c_us)
+    t += allreduce_us(xb["critic_rest"], n, eff)
+    t += max(0.0, allreduce_us(xb["actor_dW2"], n, eff) - win_a_us)
+    t += allreduce_us(xb["actor_rest"], n, eff)
+    return t
+
+
+def per_rank_step(cfg_name, device, n, mode, rb, dtype, steps=30, warmup=5, prof_steps=5):
+    """One GPU runs rank 0's workload of an n-GPU run (bench.py --per-rank-of):
+    per-rank batch B/n (strong) or B (weak), global draw of the full batch,
+    the proxy communicator (every RCCL call site, the same graph-captured
+    issue).  Returns the measured step and the exchange-overlap windows."""
+    B0 = CONFIGS[cfg_name][4]
+    b = B0 // n if mode == "strong" else B0
+    sess, _, fl, _ = build_learner(cfg_name, device, 0, n, 0, dtype=dtype, per_gpu_b=b, rb=rb,
+                                   proxy=True)
+    el = timed(fl, sess, steps, warmup, 1)
+    rows, _ = kernel_profile(fl, sess, prof_steps)
+    sess.close()
+    win = {k.split("|", 1)[1]: 1e3 * v["ms"] / v["launches"] for k, v in rows.items()
+           if k.startswith("xwin|")}
+    busy = sum(v["ms"] for k, v in rows.items() if not k.startswith(("rccl", "xwin"))) / prof_steps
+    return {"per_rank_batch": b, "step_ms": round(1000.0 * el / steps, 4),
+            "gpu_busy_ms": round(busy, 4),
+            "window_us": {k: round(v, 1) for k, v in win.items()}}
+
+
+def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
+    """Projected N-GPU throughput from one GPU: the measured per-rank step
+    (rank 0's exact workload via the proxy communicator) + the modelled
+    exchange exposed beyond the measured overlap windows.  base_value = the
+    measured 1-GPU updates/s (no communicator)."""
+    S, A, H1, H2 = CONFIGS[cfg_name][:4]
+    xb = exchange_bytes(S, A, H1, H2)
+    out = {"model": {"xgmi_link_GBs_per_direction": XGMI_LINK_GBS, "rccl_bus_efficiency": RCCL_EFF,
+                     "rccl_latency_us": RCCL_LAT_US, "exchange_bytes": xb,
+                     "formula": "step(N) = measured per-rank step (proxy communicator, graph) "
+                                "+ sum over the 4 calls of max(0, T_ar(bytes, N) - overlap "
+                                "window); T_ar = lat + 2(N-1)/N bytes / ((N-1) link eff); "
+                                "pessimistic: eff halved"},
+           "measured_1gpu_updates_s": base_value}
+    for mode in ("strong", "weak"):
+        rows = {}
+        for n in ns:
+            m = per_rank_step(cfg_name, device, n, mode, rb, dtype)
+            wc = m["window_us"].get("critic", 0.0)
+            wa = m["window_us"].get("actor", 0.0)
+            ex = exposed_exchange_us(xb, wc, wa, n)
+            ex_p = exposed_exchange_us(xb, wc, wa, n, RCCL_EFF / 2)
+            step = m["step_ms"] + ex / 1000.0
+            step_p = m["step_ms"] + ex_p / 1000.0
+            # strong: global updates/s; weak: batch-B updates processed by all ranks / s
+            val = (1.0 if mode == "strong" else n) * 1000.0 / step
+            val_p = (1.0 if mode == "strong" else n) * 1000.0 / step_p
+            m.update({"exposed_exchange_us": round(ex, 1), "projected_step_ms": round(step, 4),
+                      "projected_updates_s": round(val, 1),
+                      "speedup_vs_1gpu": round(val / base_value, 3),
+                      "pessimistic_speedup": round(val_p / base_value, 3)})
+            rows[str(n)] = m
+            log("[bench] projection %s %s N=%d: per-rank %.3f ms + exposed %.0f us -> x%.2f"
+                % (cfg_name, mode, n, m["step_ms"], ex, val / base_value))
+        out[mode] = rows
+    return out
 
 
 def timed(fl, sess, steps, warmup, world):
@@ -183,10 +289,12 @@ def summarize_profile(rows, steps):
         k = by_kernel.setdefault(sym, {"ms": 0.0, "launches": 0, "flops": 0.0, "bytes": 0.0})
         for f in ("ms", "launches", "flops", "bytes"):
             k[f] += r[f]
-    # the collectives' events run on the comm stream concurrently with kernels:
-    # they are neither GPU-busy time nor a roofline candidate
-    comp = {k: v for k, v in by_kernel.items() if not k.startswith("rccl")}
-    gpu_ms = sum(r["ms"] for k, r in rows.items() if not k.startswith("rccl")) / steps
+    # the collectives' events run on the comm stream concurrently with kernels,
+    # and the xwin records are exchange-overlap windows (spans of the step):
+    # neither is GPU-busy time nor a roofline candidate
+    side = ("rccl", "xwin")
+    comp = {k: v for k, v in by_kernel.items() if not k.startswith(side)}
+    gpu_ms = sum(r["ms"] for k, r in rows.items() if not k.startswith(side)) / steps
     gemm_ms = sum(r["ms"] for k, r in comp.items() if k.startswith("gemm")) / steps
     gemm_flops = sum(r["flops"] for k, r in comp.items() if k.startswith("gemm")) / steps
     dom = max(comp.items(), key=lambda kv: kv[1]["ms"])
@@ -227,6 +335,37 @@ def pmc_traffic(cfg_name, kernel, launches_per_step):
                 os.path.relpath(fn, ROOT), lps, launches_per_step)
         return round(k["traffic_bytes_per_launch"]), os.path.relpath(fn, ROOT)
     return None, None
+
+
+def kernel_peak(name):
+    """MFMA peak a kernel is rated against: bf16 operands (NP=1 twins, the
+    256 x 256 bf16 kernel) 2.5 PF; fp32 on the bf16 pipe (three-plane twins /
+    gemm_s3, six products per MAC) 2.5 PF / 6; the fp32-input MFMA 157.3 TF."""
+    if name.startswith("gemm_h256") or (name.startswith(("gemm_h", "gemm_s3")) and "NP=1" in name):
+        return PEAK_BF16_MFMA_TFLOPS
+    if name.startswith(("gemm_h", "gemm_s3")):
+        return PEAK_S3_FP32EQ_TFLOPS
+    return PEAK_FP32_MFMA_TFLOPS
+
+
+def mfma_busy_step(cfg_name, step_ms):
+    """Counter-measured MFMA busy of the whole step from the newest committed
+    PMC pass (profiles/**/*mfma_<config>.json, SQ_VALU_MFMA_BUSY_CYCLES per
+    launch x launches per step): busy cycles / (1024 SIMDs x step time x
+    2.4 GHz) -- at the peak clock, so a lower bound of the busy fraction at
+    the clock the chip held.  None when no pass is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*mfma_%s.json" % cfg_name),
+                             recursive=True))   # profiles/rN/...: newest round last
+    for fn in reversed(files):
+        try:
+            ks = json.load(open(fn))["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        cyc = sum(k["mfma_busy_cycles_per_launch"] * k["launches_per_step"] for k in ks.values())
+        return {"busy_at_2.4GHz": round(cyc / (1024 * step_ms * 1e-3 * 2.4e9), 4),
+                "source": os.path.relpath(fn, ROOT)}
+    return None
 
 
 def _cpu_model():
@@ -358,6 +497,11 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: per-GPU batch fixed at the config's B; strong: global batch "
                          "fixed at B (B/N rows per GPU)")
+    ap.add_argument("--per-rank-of", type=int, default=0, metavar="N",
+                    help="on ONE GPU, time exactly rank 0's workload of an N-GPU run (per-rank "
+                         "batch per --scaling, proxy communicator) and print its projection")
+    ap.add_argument("--no-project", action="store_true",
+                    help="skip the projected_scaling block (N=1 default runs only)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -381,6 +525,21 @@ def main():
     cfg = args.config
     dtype = args.dtype or DEFAULT_DTYPE[cfg]
     S, A, H1, H2, B0, scale, label = CONFIGS[cfg]
+    if args.per_rank_of > 1:
+        if world != 1:
+            raise SystemExit("[bench] --per-rank-of runs on one GPU")
+        n = args.per_rank_of
+        sess1, rb1, fl1, _ = build_learner(cfg, local, 0, 1, args.replay, dtype=dtype)
+        base = args.steps / timed(fl1, sess1, args.steps, args.warmup, 1)
+        sess1.close()
+        pr = projected_scaling(cfg, local, rb1, dtype, round(base, 3), ns=(n,))
+        print(json.dumps({"metric": "projected actor+critic updates/sec on %d GPUs (%s scaling, "
+                                    "rank 0's workload measured on one GPU)" % (n, args.scaling),
+                          "value": pr[args.scaling][str(n)]["projected_updates_s"],
+                          "unit": "updates/s", "n_gpus": 1, "per_rank_of": n,
+                          "scaling": args.scaling, "dtype": dtype, "config": {"workload": label},
+                          "projected_scaling": pr}), flush=True)
+        return
     strong = args.scaling == "strong"
     if strong and B0 % world:
         raise SystemExit("[bench] strong scaling: batch %d not divisible by %d GPUs" % (B0, world))
@@ -403,13 +562,10 @@ def main():
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_flops = dom["flops"] / dom["launches"]
     achieved = dom_flops / (dom_avg_ms * 1e-3) / 1e12
-    if dom_name.startswith(("gemm_h", "gemm_s3")) and "NP=1" in dom_name:
-        peak = PEAK_BF16_MFMA_TFLOPS
-    elif dom_name.startswith("gemm_s3") or dom_name.startswith("gemm_h"):
-        peak = PEAK_S3_FP32EQ_TFLOPS
-    else:
-        peak = PEAK_FP32_MFMA_TFLOPS
-    step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    peak = kernel_peak(dom_name)
+    # the pipe the step's GEMMs run on: bf16 operands at 2.5 PF; fp32 contexts
+    # on the same bf16 pipe at six plane products per MAC (2.5 PF / 6)
+    step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_S3_FP32EQ_TFLOPS
     traffic, traffic_src = (pmc_traffic(cfg, dom_name, dom["launches"] / args.profile_steps)
                             if world == 1 else (None, "PMC passes are single-GPU"))
     roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
@@ -434,7 +590,14 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B,
                    "parallelism": "dp%d" % world},
         "samples_per_s": round(world * args.steps / el * B, 1),
+        # whole-step algorithmic FLOP rate against the pipe the GEMMs use
+        # (step_peak); the fp32-peak reading beside it; the counter-measured
+        # MFMA busy of the step from the committed PMC pass
         "mfma_util_step": round(step_flops / (ms * 1e-3) / 1e12 / step_peak, 4),
+        "mfma_util_step_peak_tflops": step_peak,
+        "step_frac_vs_fp32_mfma_peak": round(step_flops / (ms * 1e-3) / 1e12
+                                             / PEAK_FP32_MFMA_TFLOPS, 4),
+        "mfma_busy_step_counter": mfma_busy_step(cfg, ms) if world == 1 else None,
         "step_tflops": round(step_flops / (ms * 1e-3) / 1e12, 2),
         "gemm_tflops": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else None,
         "gpu_busy_ms_per_step": round(gpu_ms, 4),
@@ -462,16 +625,25 @@ def main():
             k = by_kernel[key]
             hbm[key] = round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1)
     out["hbm_GBs"] = hbm
+    if world == 1 and rank == 0 and cfg in ("c3", "c5") and not args.no_project:
+        # SURVEY §7 / BASELINE: >= 6x at 8 GPUs -- rank 0's exact per-rank
+        # workload measured here (strong and weak), the exchange modelled
+        out["projected_scaling"] = projected_scaling(cfg, local, rb, dtype, round(value, 3))
 
     if world == 1 and rank == 0 and not args.no_small and cfg != "c2":
         s2, rb2, fl2, actor2 = build_learner("c2", local, 0, 1, REPLAY_ROWS)
         el2 = timed(fl2, s2, 500, 50, 1)
+        # the reference's worker synchronises every env step (action
+        # selection reads the updated actor, ddpg.py:68-70,86-113): the
+        # synchronous per-step latency is what its caller sees
+        lat2 = step_latency_percentiles(fl2, s2, 300)
         rows2, wall2 = kernel_profile(fl2, s2, 100)
         busy2 = sum(r["ms"] for r in rows2.values()) / 100
         nk2 = sum(r["launches"] for r in rows2.values()) / 100
         out["small_batch"] = {
             "workload": CONFIGS["c2"][6], "value": round(500 / el2, 1), "unit": "updates/s",
             "ms_per_step": round(1000 * el2 / 500, 4),
+            "step_latency": lat2,
             "kernels_per_step": nk2, "gpu_busy_ms_per_step": round(busy2, 4),
             "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1),
             "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
@@ -490,8 +662,7 @@ def main():
         f5 = flops_per_step(S5, A5, H15, H25, B5)
         ms5 = 1000.0 * el5 / 30
         ach5 = (d5["flops"] / d5["launches"]) / (d5["ms"] / d5["launches"] * 1e-3) / 1e12
-        pk5 = PEAK_BF16_MFMA_TFLOPS if "NP=1" in dn5 \
-            else PEAK_FP32_MFMA_TFLOPS
+        pk5 = kernel_peak(dn5)
         out["c5_bf16"] = {
             "workload": label5 + ", bf16 GEMM operands (fp32 master weights/accumulation)",
             "value": round((1 if strong else world) * 30 / el5, 3), "unit": "updates/s",
@@ -500,6 +671,7 @@ def main():
             "dtype": "bf16", "gpu_busy_ms_per_step": round(gpu5, 4),
             "step_tflops": round(f5 / (ms5 * 1e-3) / 1e12, 2),
             "mfma_util_step": round(f5 / (ms5 * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS, 4),
+            "mfma_busy_step_counter": mfma_busy_step("c5", ms5) if world == 1 else None,
             "roofline": {"bound": "mfma", "kernel": dn5, "achieved": round(ach5, 2), "peak": pk5,
                          "unit": "TFLOP/s", "frac": round(ach5 / pk5, 4),
                          "avg_launch_us": round(1e3 * d5["ms"] / d5["launches"], 2),
@@ -507,6 +679,9 @@ def main():
             "kernels": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
                             "per_step": v["launches"] / 10}
                         for k, v in sorted(bk5.items(), key=lambda kv: -kv[1]["ms"])}}
+        if world == 1 and not args.no_project:
+            out["c5_bf16"]["projected_scaling"] = projected_scaling(
+                "c5", local, rb5, "bf16", out["c5_bf16"]["value"])
         s5.close()
         sess = None
     if world == 1 and rank == 0 and not args.no_cpu:

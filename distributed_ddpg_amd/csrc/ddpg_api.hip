@@ -262,15 +262,32 @@ struct ddpg_ctx {
     bool act_planes = true;  // DDPG_ACT32=1: fp32 copies of h1 / cat / cat2 as well
     bool slots_h2d = false;  // DDPG_SLOTS_H2D=1: upload the step's slots instead of reading them in place
     int tk_rpb = 0;          // DDPG_TK_RPB=n: thin_k row tiles per block (0: auto)
+    bool kcomb = true;       // DDPG_KCOMB=0: no in-launch K split for small-M plain twin GEMMs
+    int kc_blocks = 200;     // DDPG_KCOMB_BLOCKS=n: split plain twin GEMMs of fewer tiles
   } sw;
+
+  // small-M plan (ksplit_combine, gemm_common.h): kc_rot rotating partial
+  // buffers of kc_part_n floats and ticket segments of kKcTickets, one per
+  // combined launch in issue order (launches that may run concurrently on the
+  // step's streams never share one)
+  float* kc_part = nullptr;
+  size_t kc_part_n = 0;
+  unsigned* kc_ticket = nullptr;
+  int kc_rot = 0, kc_next = 0;
 
   // comm: every collective of the ctx is issued on cs (one stream, so the
   // communicator sees them in the same order on every rank); cs forks from the
   // producing stream and joins the consumer through the cev events
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
+  int cworld = 1;  // ranks in the communicator (1 for a 1-rank or a proxy communicator)
+  // the step graph captures the collectives too (env DDPG_GRAPH_COMM=0: such
+  // steps stay eager); cleared if a capture with RCCL calls fails
+  bool comm_graph = true;
   hipStream_t cs = nullptr;
   hipEvent_t cev[8] = {};
+  int win_rec = -1;     // profiling: open exchange-overlap window (prof_recs index)
+  int test_cs_spin = 0;  // env DDPG_TEST_CS_SPIN=us (test hook, cs_spin_scale_kernel)
 
   // profiling
   bool prof = false;
@@ -280,6 +297,7 @@ struct ddpg_ctx {
 };
 
 static constexpr int kSlotRing = 4;
+static constexpr int kKcTickets = 1024;  // ticket segment (output tiles) per combined launch
 static constexpr int kHeadRows = 64, kHeadRows4 = 64;
 
 // ---------------------------------------------------------------- profiling helpers
@@ -630,6 +648,29 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
         h.direct = true;
       }
       GemmHArgs a;
+      // small-M plan: a plain GEMM (forward / dX) whose tiles leave most CUs
+      // idle -- per-rank batches of a strong-scaling run, e.g. C3 at B = 512
+      // has 32 forward tiles for 256 CUs -- splits K over ~256 blocks (>= 3
+      // k-tiles each) and combines the splits in-launch before its epilogue
+      // (ksplit_combine).  The immediate-offset kernels only.
+      const bool kc_kernel = c->sw.gemm_h3 && (c->hnp == 3 || (c->hnp == 1 && c->sw.gemm_mf == 16 &&
+                                                              AL == L_RK));
+      if (splits_req == 1 && kc_kernel && c->kc_part) {
+        const int tiles = h.nt(N) * h.mt(M);
+        const int nkt = Kh / BKh;
+        int sk = std::min(ceil_div(256, tiles), nkt / 3);
+        if (tiles < c->sw.kc_blocks && sk >= 2) {
+          const int kps = ceil_div(nkt, sk) * BKh;
+          sk = ceil_div(Kh, kps);
+          if (sk >= 2 && (size_t)sk * tiles * BMh * HG_BN <= c->kc_part_n && tiles <= kKcTickets) {
+            const int slot = c->kc_next++ % c->kc_rot;
+            a.kpart = c->kc_part + (size_t)slot * c->kc_part_n;
+            a.kticket = c->kc_ticket + (size_t)slot * kKcTickets;
+            h.kps = kps;
+            h.splits = sk;
+          }
+        }
+      }
       a.A = ta.p;
       a.B = tb.p;
       a.pa = ta.ps;
@@ -687,10 +728,11 @@ static GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int l
       // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
       const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
       char key[112];
-      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s",
+      // "/kc": the splits are combined in-launch (small-M plan)
+      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s%s",
                h16 ? (AL == L_RK && c->sw.gemm_h3 ? "gemm_h16i_kernel" : "gemm_h16_kernel")
                    : (c->hnp == 3 && c->sw.gemm_h3) ? "gemm_h3_kernel" : "gemm_h_kernel",
-               lay[AL], lay[BL], c->hnp, name);
+               lay[AL], lay[BL], c->hnp, name, a.kpart ? "/kc" : "");
       ProfScope ps(c, key, 2.0 * M * N * (double)K,
                    2.0 * c->hnp * ((double)M * K + (double)K * N) +
                        4.0 * (double)M * N * h.splits);
@@ -1190,14 +1232,31 @@ static void cs_link(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
 // with_stats: the all-gather of the step's {q_max, loss} joins the same group
 // (one collective launch, one latency on the critical path instead of two);
 // stats_allreduce_on_cs then only reduces the gathered values.
+// window (profiling only): open an exchange-overlap record on the producing
+// stream, closed by the next join_cs -- the compute that stream runs between
+// issuing this exchange and waiting for it (bench.py's projected scaling).
 static void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0,
-                            float* b1 = nullptr, size_t n1 = 0, bool with_stats = false) {
+                            float* b1 = nullptr, size_t n1 = 0, bool with_stats = false,
+                            const char* window = nullptr) {
   if (!c->comm) return;
   cs_link(c, ev, c->cur, c->cs);
   const hipStream_t prev = c->cur;
+  if (window && c->prof && c->win_rec < 0) {
+    ProfRec rec{window, ev_get(c), ev_get(c), 0.0, (double)n0 * 4.0};
+    HIP_TRY(hipEventRecord(rec.e0, prev));
+    c->prof_recs.push_back(rec);
+    c->win_rec = (int)c->prof_recs.size() - 1;
+  }
   c->cur = c->cs;
+  if (c->test_cs_spin) {
+    // test hook: the exchanged ranges doubled after a delay, on cs ahead of
+    // the group -- a consumer not ordered behind cs reads them undoubled
+    hipLaunchKernelGGL(cs_spin_scale_kernel, dim3(256), dim3(256), 0, c->cs, b0, (long long)n0,
+                       b1, (long long)n1, c->test_cs_spin);
+    HIP_TRY(hipGetLastError());
+  }
   {
-    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0 + (with_stats ? 8.0 * c->world : 0.0));
+    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0 + (with_stats ? 8.0 * c->cworld : 0.0));
     nccl_try(ncclGroupStart());
     if (n0) nccl_try(ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs));
     if (n1) nccl_try(ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs));
@@ -1219,10 +1278,10 @@ static void stats_allreduce_on_cs(ddpg_ctx* c, bool gathered = false) {
   const hipStream_t prev = c->cur;
   c->cur = c->cs;
   {
-    ProfScope ps(c, "rccl_stats", 0, gathered ? 0.0 : 8.0 * c->world);
+    ProfScope ps(c, "rccl_stats", 0, gathered ? 0.0 : 8.0 * c->cworld);
     if (!gathered)
       nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
-    hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cs, c->dstats_all, c->world,
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cs, c->dstats_all, c->cworld,
                        c->dstats, c->dacc);
     HIP_TRY(hipGetLastError());
   }
@@ -1231,7 +1290,12 @@ static void stats_allreduce_on_cs(ddpg_ctx* c, bool gathered = false) {
 
 // the consumer stream (c->cur) waits for every collective queued on cs
 static void join_cs(ddpg_ctx* c, int ev) {
-  if (c->comm) cs_link(c, ev, c->cs, c->cur);
+  if (!c->comm) return;
+  if (c->win_rec >= 0) {  // close the exchange-overlap window on the consumer stream
+    HIP_TRY(hipEventRecord(c->prof_recs[c->win_rec].e1, c->cur));
+    c->win_rec = -1;
+  }
+  cs_link(c, ev, c->cs, c->cur);
 }
 
 // TF ApplyAdam over one network's flat region.  advance: also advance its
@@ -1355,7 +1419,8 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
     t1.nseg = 0;
     add_wgrad(t1, pWh, c->slab_Wh, G + L.c[CWH].off, nWh);
     if (t1.nseg) reduce_launch(c, "grad_reduce", t1);
-    allreduce_on_cs(c, 0, "rccl_allreduce", G + L.c[CWH].off, (size_t)nWh);
+    allreduce_on_cs(c, 0, "rccl_allreduce", G + L.c[CWH].off, (size_t)nWh, nullptr, 0, false,
+                    "xwin|critic");
   }
   c->cur = main;
   // dcat = dh_pre . Wh^T * elu'(cat);  column sums -> [dbs | dba]
@@ -1473,7 +1538,8 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
     t1.nseg = 0;
     add_wgrad(t1, pW2, c->slab_W2, G + L.a[AW2].off, nW2);
     if (t1.nseg) reduce_launch(c, "grad_reduce", t1);
-    allreduce_on_cs(c, 3, "rccl_allreduce", G + L.a[AW2].off, (size_t)nW2);
+    allreduce_on_cs(c, 3, "rccl_allreduce", G + L.a[AW2].off, (size_t)nW2, nullptr, 0, false,
+                    "xwin|actor");
   }
   c->cur = main;
   // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
@@ -1799,7 +1865,7 @@ static void ctx_free(ddpg_ctx* c) {
   for (void* p : {(void*)c->sb_save, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T,
                   (void*)c->sb_stamps})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)c->atw, (void*)c->wtw})
+  for (void* p : {(void*)c->atw, (void*)c->wtw, (void*)c->kc_part, (void*)c->kc_ticket})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc, (void*)c->dstats_all})
@@ -1929,6 +1995,11 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.act_planes = !env_is("DDPG_ACT32", "1");
       c->sw.slots_h2d = env_is("DDPG_SLOTS_H2D", "1");
       if (const char* v = getenv("DDPG_TK_RPB")) c->sw.tk_rpb = std::max(0, atoi(v));
+      c->sw.kcomb = !env_is("DDPG_KCOMB", "0");
+      if (const char* v = getenv("DDPG_KCOMB_BLOCKS"))
+        c->sw.kc_blocks = std::min(kKcTickets, std::max(1, atoi(v)));
+      if (const char* v = getenv("DDPG_TEST_CS_SPIN")) c->test_cs_spin = std::max(0, atoi(v));
+      if (env_is("DDPG_GRAPH_COMM", "0")) c->comm_graph = false;
     }
     c->split_cap_W1 = make_plan(c->S, c->AH1, c->Bmax, 0).splits;
     c->split_cap_W2 = make_plan(c->AH1, c->AH2, c->Bmax, 0).splits;
@@ -2019,6 +2090,17 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     if (const char* gv = getenv("DDPG_GRAPH")) c->use_graph = atoi(gv) != 0;
     if (const char* gv = getenv("DDPG_GRAPH_AUTO")) c->graph_auto = atoi(gv) != 0;
     if (const char* pv = getenv("DDPG_PAR")) c->par = atoi(pv) != 0;
+    if (c->hnp && c->sw.kcomb) {
+      // a combined launch has S x tiles < 256 + kc_blocks blocks of BM x 128
+      // partials; two buffers suffice on one stream, eight cover the
+      // concurrent branches of DDPG_PAR=1
+      const int BMh = c->hnp == 1 ? 256 : 128;
+      c->kc_rot = c->par ? 8 : 2;
+      c->kc_part_n = (size_t)(256 + c->sw.kc_blocks) * BMh * HG_BN;
+      HIP_TRY(hipMalloc(&c->kc_part, c->kc_rot * c->kc_part_n * sizeof(float)));
+      HIP_TRY(hipMalloc(&c->kc_ticket, (size_t)c->kc_rot * kKcTickets * sizeof(unsigned)));
+      HIP_TRY(hipMemset(c->kc_ticket, 0, (size_t)c->kc_rot * kKcTickets * sizeof(unsigned)));
+    }
     {
       const int hmax = std::max(std::max(c->AH1, c->AH2), std::max(c->CH1, c->CH2));
       const int LX = rup(std::max(c->S, c->A), 4);
@@ -2743,22 +2825,24 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   // the small path reads no twins: they are rebuilt lazily by the next
   // large-batch call (every 1:1 method and large step calls twins_refresh)
   if (!small) twins_refresh(c);
-  // graphs: single-rank, not profiling (RCCL capture and per-kernel events stay eager)
+  // graphs: not profiling (per-kernel events stay eager); a data-parallel
+  // step captures its RCCL calls as graph nodes (DDPG_GRAPH_COMM=0: eager)
   bool idle = true;  // the previous step has finished (never-recorded event: success)
   if (c->graph_auto && small) {
     const hipError_t q = hipEventQuery(c->step_done);
     if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
     idle = q == hipSuccess;
   }
-  if (c->use_graph && idle && c->world == 1 && !c->comm && !c->prof) {
+  const bool graph_ok = c->comm ? c->comm_graph : c->world == 1;
+  bool graphed = false;
+  if (c->use_graph && idle && graph_ok && !c->prof) {
     auto& g = c->gslot[c->gcur];
-    c->gcur ^= 1;
     HIP_TRY(hipEventSynchronize(g.done));  // this slot's previous replay has finished
     for (int i = 0; i < B; ++i) g.h_idx[i] = pos_to_slot(rb, mine[i]);
     if (!g.exec || g.B != B || g.rb != rb || g.scaler != c->has_scaler) {
       if (g.exec) HIP_TRY(hipGraphExecDestroy(g.exec));
       g.exec = nullptr;
-      hipGraph_t graph;
+      hipGraph_t graph = nullptr;
       HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
       try {
         if (c->sw.slots_h2d) {
@@ -2771,21 +2855,44 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
         }
         learner_step_any(c, rb, B, inv_b);
         c->slots_src = nullptr;
-      } catch (...) {
+        HIP_TRY(hipStreamEndCapture(c->stream, &graph));
+        HIP_TRY(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+        HIP_TRY(hipGraphDestroy(graph));
+        graph = nullptr;
+      } catch (const DdpgError& e) {
         c->slots_src = nullptr;
-        (void)hipStreamEndCapture(c->stream, &graph);
-        throw;
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(c->stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
+          hipGraph_t dead = nullptr;
+          (void)hipStreamEndCapture(c->stream, &dead);
+          if (dead) (void)hipGraphDestroy(dead);
+        }
+        if (graph) (void)hipGraphDestroy(graph);
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        g.exec = nullptr;
+        (void)hipGetLastError();
+        if (!c->comm) throw;
+        // RCCL calls did not capture here: this ctx runs its steps eagerly
+        c->comm_graph = false;
+        c->cur = c->stream;
+        c->td_nqt = 0;
+        fprintf(stderr, "[ddpg] step graph with RCCL calls failed (%s); eager steps\n",
+                e.msg.c_str());
       }
-      HIP_TRY(hipStreamEndCapture(c->stream, &graph));
-      HIP_TRY(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
-      HIP_TRY(hipGraphDestroy(graph));
-      g.B = B;
-      g.rb = rb;
-      g.scaler = c->has_scaler;
+      if (g.exec) {
+        g.B = B;
+        g.rb = rb;
+        g.scaler = c->has_scaler;
+      }
     }
-    HIP_TRY(hipGraphLaunch(g.exec, c->stream));
-    HIP_TRY(hipEventRecord(g.done, c->stream));
-  } else {
+    if (g.exec) {
+      c->gcur ^= 1;
+      HIP_TRY(hipGraphLaunch(g.exec, c->stream));
+      HIP_TRY(hipEventRecord(g.done, c->stream));
+      graphed = true;
+    }
+  }
+  if (!graphed) {
     const int si = c->slot_i;
     c->slot_i = (c->slot_i + 1) % kSlotRing;
     HIP_TRY(hipEventSynchronize(c->slot_ev[si]));
@@ -2860,6 +2967,17 @@ int ddpg_read_stats(ddpg_ctx* c, double* qsum, double* lsum, int64_t* steps, int
 }
 
 // ---------------------------------------------------------------- comm
+// comm stream, its events and the stats all-gather buffer for a communicator
+// of `cworld` ranks
+static void comm_setup(ddpg_ctx* c, int cworld) {
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)cworld * sizeof(float)));
+  if (!c->cs) HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  for (auto& ev : c->cev)
+    if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+}
+
 int ddpg_comm_unique_id(char* out128) {
   ncclUniqueId id;
   ncclResult_t r = ncclGetUniqueId(&id);
@@ -2882,13 +3000,20 @@ int ddpg_comm_init(ddpg_ctx* c, const char* id128, int world, int rank) {
     // runs (as an identity) through the same RCCL call sites as world > 1
     ncclUniqueId id;
     memcpy(&id, id128, 128);
-    HIP_TRY(hipSetDevice(c->cfg.device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)world * sizeof(float)));
-    if (!c->cs) HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
-    for (auto& ev : c->cev)
-      if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    comm_setup(c, world);
     nccl_try(ncclCommInitRank(&c->comm, world, id, rank));
+    c->cworld = world;
+  });
+}
+
+int ddpg_comm_init_proxy(ddpg_ctx* c) {
+  return guard(c, [&] {
+    if (c->comm) throw DdpgError(DDPG_ESTATE, "communicator already initialised");
+    ncclUniqueId id;
+    nccl_try(ncclGetUniqueId(&id));
+    comm_setup(c, 1);
+    nccl_try(ncclCommInitRank(&c->comm, 1, id, 0));
+    c->cworld = 1;
   });
 }
 

@@ -400,4 +400,72 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   }
 }
 
+// ---------------------------------------------------------------- in-launch K split
+// Small-M plan (per-rank batches of a strong-scaling run: M = B <= 2048): a
+// plain GEMM whose output tiles do not fill the chip runs its K range as
+// gridDim.z splits, and the splits of each tile are combined inside the same
+// launch before the fused epilogue.  Every block stores its fp32 partial
+// (each lane's accumulator registers as 64-B runs: coalesced) to its slot of
+// `part` ([tile][split][NV][threads][16]), then takes a ticket on the tile;
+// the block that draws the last ticket adds the partials in split order
+// 0 .. S-1 (its own from registers), so the sum does not depend on which
+// split arrives last (bitwise reproducible), resets the ticket for the next
+// launch and returns true; the other blocks return false and exit.
+// Visibility across XCDs (each has its own L2): agent-scope release before
+// the ticket (the partial stores written back), acquire after it.
+template <int NV>
+DDPG_DEV bool ksplit_combine(f32x16* acc, float* part, unsigned* ticket, int tile, int z, int S,
+                             int tid, int nt) {
+  __shared__ unsigned last_s;
+  const size_t slab = (size_t)NV * nt * 16;
+  float* base = part + (size_t)tile * S * slab;
+  {
+    float* mine = base + (size_t)z * slab;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      float4* o = reinterpret_cast<float4*>(mine + ((size_t)v * nt + tid) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        o[q] = make_float4(acc[v][4 * q], acc[v][4 * q + 1], acc[v][4 * q + 2], acc[v][4 * q + 3]);
+    }
+  }
+  __threadfence();  // release: this thread's partial is visible device-wide
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old =
+        __hip_atomic_fetch_add(ticket + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned l = old == (unsigned)(S - 1);
+    if (l) __hip_atomic_store(ticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = l;
+  }
+  __syncthreads();
+  if (!last_s) return false;
+  __threadfence();  // acquire: the other splits' partials
+  f32x16 own[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) own[v] = acc[v];
+  for (int zz = 0; zz < S; ++zz) {
+    const float* src = base + (size_t)zz * slab;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f32x16 p;
+      if (zz == z) {
+        p = own[v];
+      } else {
+        const float4* s4 = reinterpret_cast<const float4*>(src + ((size_t)v * nt + tid) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 x = s4[q];
+          p[4 * q] = x.x;
+          p[4 * q + 1] = x.y;
+          p[4 * q + 2] = x.z;
+          p[4 * q + 3] = x.w;
+        }
+      }
+      acc[v] = zz == 0 ? p : acc[v] + p;
+    }
+  }
+  return true;
+}
+
 }  // namespace ddpg

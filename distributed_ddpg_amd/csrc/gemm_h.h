@@ -47,6 +47,11 @@ struct GemmHArgs {
   int kps;  // k extent per split (multiple of BK)
   int xcd;
   GemmEpi e;
+  // in-launch K split (ksplit_combine, gemm_h3_kernel / gemm_h16i_kernel):
+  // partials [tile][split] and one ticket per output tile; null: the splits
+  // are separate slabs (weight gradients) or there is one split
+  float* kpart = nullptr;
+  unsigned* kticket = nullptr;
 };
 
 constexpr int HG_NT = 512, HG_BN = 128, HG_STAGES = 3;

@@ -267,12 +267,19 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) acc[i][0] += acs[i][0];
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  int ze = z;
+  if (g.kpart) {  // small-M plan: this launch's splits are combined here
+    if (!ksplit_combine<TM>(&acc[0][0], g.kpart, g.kticket, by * gridDim.x + bx, z, gridDim.z,
+                            tid, HG_NT))
+      return;
+    ze = 0;
+  }
   __syncthreads();  // staging buffers are reused by the epilogue
   GemmArgs ge;
   ge.M = g.M;
   ge.N = g.N;
   ge.e = g.e;
-  gemm_epilogue<BM, HG_BN, WGN>(acc, smem, ge, tid, n0, m0, z, bx, by);
+  gemm_epilogue<BM, HG_BN, WGN>(acc, smem, ge, tid, n0, m0, ze, bx, by);
 }
 
 }  // namespace ddpg
@@ -484,12 +491,19 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_kernel(GemmHArgs g) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) out[i][0][4 * (2 * tr + tc) + q] = acc[2 * i + tr][tc][q];
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  int ze = z;
+  if (g.kpart) {  // small-M plan: this launch's splits are combined here
+    if (!ksplit_combine<TM>(&out[0][0], g.kpart, g.kticket, by * gridDim.x + bx, z, gridDim.z,
+                            tid, HG_NT))
+      return;
+    ze = 0;
+  }
   __syncthreads();  // staging buffers are reused by the epilogue
   GemmArgs ge;
   ge.M = g.M;
   ge.N = g.N;
   ge.e = g.e;
-  gemm_epilogue<BM, HG_BN, 4, 16>(out, smem, ge, tid, n0, m0, z, bx, by);
+  gemm_epilogue<BM, HG_BN, 4, 16>(out, smem, ge, tid, n0, m0, ze, bx, by);
 }
 
 }  // namespace ddpg

@@ -116,6 +116,21 @@ __global__ void stats_reduce_kernel(const float* __restrict__ all, int world,
   }
 }
 
+// Test hook of the data-parallel ordering (env DDPG_TEST_CS_SPIN=us; the
+// comm stream, ahead of a collective group): every block waits `us`
+// microseconds of wall clock (100 MHz s_memrealtime), then the grid doubles
+// the two gradient ranges the group exchanges (exact in fp32).  A reader not
+// ordered behind the comm stream would see the undoubled values.
+__global__ void cs_spin_scale_kernel(float* b0, long long n0, float* b1, long long n1, int us) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned long long)us)
+    __builtin_amdgcn_s_sleep(8);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long long i = i0; i < n0; i += stride) b0[i] = 2.f * b0[i];
+  for (long long i = i0; i < n1; i += stride) b1[i] = 2.f * b1[i];
+}
+
 // ---------------------------------------------------------------- thin heads
 // actor output: o = tanh(sum_t part[t][b][a]); mu = o * scale  (networks.py:59-61)
 __global__ void actor_out_kernel(const float* __restrict__ part, int NT, int B, int A,

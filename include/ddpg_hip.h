@@ -212,12 +212,20 @@ int ddpg_comm_unique_id(char* out128);
 /* Replaces tf.train.ClusterSpec/Server + replica_device_setter (ddpg.py:168-174).
  * world/rank must equal the cfg's.  world == 1 creates a 1-rank communicator:
  * the step then runs its exchanges through the same RCCL call sites (identity
- * sums), eagerly and on the large-batch path -- a test of those call sites on
- * one GPU; without a communicator a world == 1 ctx issues no collectives.
+ * sums) on the large-batch path -- a test of those call sites on one GPU;
+ * without a communicator a world == 1 ctx issues no collectives.
  * The exchanges run on a library-owned comm stream: the dWh (critic) and dW2
  * (actor) all-reduces start as soon as those gradients are reduced, under the
- * remaining backward GEMMs; each network's Adam waits for its exchange. */
+ * remaining backward GEMMs; each network's Adam waits for its exchange.  The
+ * step's hipGraph captures the RCCL calls with the kernels (env
+ * DDPG_GRAPH_COMM=0, or a failed capture, keeps such steps eager). */
 int ddpg_comm_init(ddpg_ctx* ctx, const char* id128, int world, int rank);
+/* Measurement hook (bench.py --per-rank-of): a 1-rank communicator standing in
+ * for the cfg.world-rank one, so that ONE GPU runs exactly rank cfg.rank's
+ * share of a cfg.world-rank step -- its slice of the global draw, every RCCL
+ * call site (as identities), the same issue path -- for timing.  Gradients are
+ * then this rank's partial sums, not the global ones. */
+int ddpg_comm_init_proxy(ddpg_ctx* ctx);
 
 /* ------------------------------------------------------------- profiling */
 /* Enable per-kernel HIP-event timing on the ctx stream (0 disables). */

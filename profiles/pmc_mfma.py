@@ -20,6 +20,17 @@ in which its matrix core was busy.  It differs from the FLOP-derived fraction
 in bench.py's roofline by the clock: that one divides by the 2.4 GHz peak,
 this one by the dispatch's own cycles (effective clock = GRBM_GUI_ACTIVE / 8 /
 duration, reported too).
+
+On short dispatches GRBM_GUI_ACTIVE over-counts (the implied clock exceeds
+the 2.4 GHz peak: MI355X_MICROARCH.md's short-dispatch caveat), so the
+GRBM-based quotient is not evidence there.  Every kernel therefore also gets
+
+  busy_at_peak_clock = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x duration x 2.4 GHz)
+
+(the dispatch's own duration from the same pass), a lower bound of the busy
+fraction at any clock <= 2.4 GHz, and `busy_fraction` is the GRBM quotient only
+where its implied clock is <= 2.4 GHz, else busy_at_peak_clock (`basis` says
+which).
 """
 import collections
 import csv
@@ -31,6 +42,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_traffic import bench_name  # noqa: E402
 
 N_SIMD, N_XCD = 1024, 8
+PEAK_GHZ = 2.4
 
 
 def main(pmc_dir, config, steps):
@@ -60,10 +72,16 @@ def main(pmc_dir, config, steps):
                "grbm_gui_active_per_launch": gr,
                "busy_fraction": mb / (N_SIMD * gr / N_XCD)}
         durs = [durations[(k, d)] for d in disp if (k, d) in durations]
+        ent["basis"] = "GRBM_GUI_ACTIVE"
         if durs:
             ns = sum(durs) / len(durs)
             ent["avg_duration_us"] = ns / 1e3
             ent["effective_clock_GHz"] = (gr / N_XCD) / ns
+            ent["busy_at_peak_clock"] = mb / (N_SIMD * ns * PEAK_GHZ)
+            if ent["effective_clock_GHz"] > PEAK_GHZ:
+                ent["busy_fraction_grbm"] = ent["busy_fraction"]
+                ent["busy_fraction"] = ent["busy_at_peak_clock"]
+                ent["basis"] = "duration x 2.4 GHz (GRBM clock above peak)"
         out["kernels"][k] = ent
     json.dump(out, sys.stdout, indent=1)
     print()

@@ -146,13 +146,13 @@ def trajectory(meta, ckpt, graph, batch_fn, steps, fresh=False, scaler=None):
     return fx
 
 
-def ip_batch(rng):
+def ip_batch(rng, b=B):
     """An InvertedPendulum-like batch as the reference's replay returns it."""
-    s = rng.normal(0, 0.2, (B, 4))
-    s2 = s + rng.normal(0, 0.02, (B, 4))
-    a = rng.uniform(-3, 3, (B, 1)).astype(np.float32)
-    r = np.ones(B)
-    t = rng.random(B) < 0.1
+    s = rng.normal(0, 0.2, (b, 4))
+    s2 = s + rng.normal(0, 0.02, (b, 4))
+    a = rng.uniform(-3, 3, (b, 1)).astype(np.float32)
+    r = np.ones(b)
+    t = rng.random(b) < 0.1
     return s, a, r, t, s2
 
 
@@ -194,6 +194,14 @@ def main():
         len(fx), STEPS, [float(fx["final/" + k]) for k in POWERS]))
     # the MountainCar graph (S=2, actor 48/64, critic 48/128) from its own
     # checkpoint (t ~ 45k Adam steps), states through the fitted scaler
+    # the reference's default batch (parameters.py:11, 256): the same graph and
+    # checkpoint, 3 steps of 256 rows -- on the GPU this runs through the
+    # large-batch GEMM path (DDPG_SMALL=0), pinning the twin GEMMs, their
+    # in-launch K split and the slab reductions to the executed graph directly
+    fx = trajectory(REF, REF, "ip", lambda rng: ip_batch(rng, 256), STEPS)
+    np.savez_compressed(os.path.join(HERE, "graph_ip1410_b256.npz"), **fx)
+    print("graph_ip1410_b256.npz: %d arrays, loss per step %s" % (
+        len(fx), [float(fx["step%d/loss" % i]) for i in range(STEPS)]))
     fx = trajectory(MC, MC, "mc", mc_batch, STEPS, scaler=mc_scaler())
     np.savez_compressed(os.path.join(HERE, "graph_mc120.npz"), **fx)
     print("graph_mc120.npz: %d arrays, loss per step %s" % (

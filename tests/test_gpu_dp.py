@@ -1,0 +1,233 @@
+"""GPU tests of the per-rank data-parallel path on one GPU:
+
+  * the small-M plan (in-launch K split of the forward / dX twin GEMMs,
+    ksplit_combine) at a strong-scaling per-rank batch of the headline shape
+    (C3 widths, B = 512: rank 0 of 8) against the oracle, graph vs eager bitwise;
+  * DDPG_KCOMB=0 (no in-launch split) against the oracle;
+  * the proxy communicator (ddpg_comm_init_proxy): one GPU runs rank 0's share
+    of an 8-rank step -- its slice of the global draw, every RCCL call site --
+    checked against the oracle on that slice; the step graph with the RCCL
+    calls captured equals the eager step bitwise;
+  * the comm-stream ordering (DDPG_TEST_CS_SPIN): a kernel on the comm stream
+    that waits, then doubles the exchanged gradient ranges; Adam must see the
+    doubled values (profiling off, graph and eager, one and three streams).
+
+Bars as tests/test_gpu_configs.py: gradients / Adam slots 1e-4 (fp32).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from test_gpu_configs import _noisy_params, _open, _rows
+from test_gpu_parity import CONFIGS, GRAD_TOL, _fill, _params, _session, rel
+
+pytestmark = pytest.mark.gpu
+
+ENV = ("DDPG_KCOMB", "DDPG_KCOMB_BLOCKS", "DDPG_GRAPH", "DDPG_GRAPH_COMM", "DDPG_PAR",
+       "DDPG_TEST_CS_SPIN", "DDPG_SMALL")
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import ddpg_oracle
+    return ddpg_oracle
+
+
+@pytest.fixture(scope="module")
+def dd():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import distributed_ddpg_amd.networks as nets
+    return nets
+
+
+@pytest.fixture
+def clean_env(monkeypatch):
+    for k in ENV:
+        monkeypatch.delenv(k, raising=False)
+    return monkeypatch
+
+
+def _state(sess):
+    from distributed_ddpg_amd import _lib
+    return [sess.get_params(w) for w in (_lib.ACTOR, _lib.CRITIC, _lib.ACTOR_TARGET,
+                                         _lib.CRITIC_TARGET, _lib.ACTOR_ADAM_M, _lib.ACTOR_ADAM_V,
+                                         _lib.CRITIC_ADAM_M, _lib.CRITIC_ADAM_V, _lib.ACTOR_GRAD,
+                                         _lib.CRITIC_GRAD)]
+
+
+def _same(a, b):
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert np.array_equal(u, v)
+
+
+C3 = (64, 16, 1024, 1024, 1.0)
+
+
+def _c3_run(dd, O, p, rows, B, Bg, world=1, proxy=False, profile=False, critic_lr=1e-3,
+            seed=77):
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale = C3
+    sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B, rank=0, world=world,
+                                critic_lr=critic_lr)
+    if proxy:
+        _lib.check(_lib.lib.ddpg_comm_init_proxy(sess.ctx), sess.ctx)
+    rb = ReplayBuffer(len(rows[0]) + 1000, seed)
+    rb.add_batch(*rows)
+    fl = FusedLearner(sess, rb, Bg)
+    prof = Profile(sess)
+    if profile:
+        prof.enable(True)
+    st = fl.step(stats=True)
+    keys = sorted(prof.read()) if profile else []
+    if profile:
+        prof.enable(False)
+    out = _state(sess), st, keys
+    sess.close()
+    return out
+
+
+def test_small_m_plan_c3_b512(dd, O, clean_env):
+    """C3 widths at B = 512 (the per-rank batch of an 8-GPU strong-scaling
+    run): the forward and dX twin GEMMs (32 / 32-64 output tiles) split K
+    and combine in-launch.  One fused step: every gradient and the Adam slots
+    at 1e-4 of the float64 oracle; the graph replay and the profiled eager
+    step are bitwise equal (the combine sums the splits in a fixed order)."""
+    S, A, H1, H2, scale = C3
+    B = 512
+    p = _noisy_params(O, S, A, H1, H2, seed=50)
+    rows = _rows(np.random.default_rng(9), 6000, S, A, scale)
+    g_state, g_st, _ = _c3_run(dd, O, p, rows, B, B)
+    e_state, e_st, keys = _c3_run(dd, O, p, rows, B, B, profile=True)
+    assert any(k.startswith("gemm_h3_kernel<RK,KR") and k.endswith("/kc") for k in keys), keys
+    assert any(k.startswith("gemm_h3_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
+    _same(g_state, e_state)
+    assert g_st == e_st
+    idx = np.array(random.Random(77).sample(range(6000), B))
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    assert abs(g_st[1] - float(out["loss"])) <= GRAD_TOL * abs(float(out["loss"]))
+    for gi, mi, vi, ref, keys_ in ((9, 6, 7, out["critic_grads"], O.CRITIC_KEYS),
+                                   (8, 4, 5, out["actor_grads"], O.ACTOR_KEYS)):
+        for k, g, m, v in zip(keys_, g_state[gi], g_state[mi], g_state[vi]):
+            r = ref[k].reshape(g.shape)
+            assert rel(g, r) < GRAD_TOL, ("grad", k, rel(g, r))
+            assert rel(m, 0.1 * r) < GRAD_TOL, ("m", k)
+            assert rel(v, 0.001 * r * r) < 2 * GRAD_TOL, ("v", k)
+
+
+def test_kcomb_off_matches_oracle(dd, O, clean_env):
+    """DDPG_KCOMB=0: the same small-M GEMMs unsplit (32 blocks each) --
+    no "/kc" launches, and the 1e-4 gradient bars hold."""
+    S, A, H1, H2, scale = C3
+    B = 512
+    clean_env.setenv("DDPG_KCOMB", "0")
+    p = _noisy_params(O, S, A, H1, H2, seed=51)
+    rows = _rows(np.random.default_rng(10), 6000, S, A, scale)
+    state, st, keys = _c3_run(dd, O, p, rows, B, B, profile=True)
+    assert not any(k.endswith("/kc") for k in keys), keys
+    idx = np.array(random.Random(77).sample(range(6000), B))
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    for gi, ref, keys_ in ((9, out["critic_grads"], O.CRITIC_KEYS),
+                           (8, out["actor_grads"], O.ACTOR_KEYS)):
+        for k, g in zip(keys_, state[gi]):
+            assert rel(g, ref[k].reshape(g.shape)) < GRAD_TOL, ("grad", k)
+
+
+def test_proxy_rank0_of_8_c3(dd, O, clean_env):
+    """bench.py --per-rank-of 8 (strong): world = 8, rank 0, per-rank batch
+    512 of a global 4096 draw, proxy communicator.  The step samples the
+    global batch, gathers rank 0's slice and runs every RCCL call site (a
+    1-rank identity).  critic_lr = 0 keeps the critic fixed, so: the critic
+    gradient = the oracle's mean over the slice x 512/4096 (the loss is scaled
+    by 1/B_global), the actor gradient = the oracle's batch sum over the slice,
+    the loss share = the slice loss / 8.  The graph with the RCCL calls
+    captured and the eager step (DDPG_GRAPH_COMM=0) are bitwise equal."""
+    S, A, H1, H2, scale = C3
+    B, Bg, world = 512, 4096, 8
+    p = _noisy_params(O, S, A, H1, H2, seed=52)
+    rows = _rows(np.random.default_rng(11), 9000, S, A, scale)
+    g_state, g_st, _ = _c3_run(dd, O, p, rows, B, Bg, world=world, proxy=True, critic_lr=0.0)
+    clean_env.setenv("DDPG_GRAPH_COMM", "0")
+    e_state, e_st, keys = _c3_run(dd, O, p, rows, B, Bg, world=world, proxy=True,
+                                  critic_lr=0.0, profile=True)
+    assert "rccl_allreduce" in keys and "rccl_stats" in keys, keys
+    assert any(k.startswith("xwin|") for k in keys), keys
+    _same(g_state, e_state)
+    assert g_st == e_st
+    idx = np.array(random.Random(77).sample(range(9000), Bg))[:B]
+    L = O.Learner(S, A, H1, H2, scale, critic_lr=0.0, dtype=np.float64, params=p,
+                  init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    assert abs(g_st[1] - float(out["loss"]) / world) <= GRAD_TOL * abs(float(out["loss"]) / world)
+    assert abs(g_st[0] - float(np.max(out["q"]))) <= 1e-5 * max(1.0, abs(float(np.max(out["q"]))))
+    for gi, ref, keys_, f in ((9, out["critic_grads"], O.CRITIC_KEYS, 1.0 / world),
+                              (8, out["actor_grads"], O.ACTOR_KEYS, 1.0)):
+        for k, g in zip(keys_, g_state[gi]):
+            assert rel(g, f * ref[k].reshape(g.shape)) < GRAD_TOL, ("grad", k)
+
+
+def _wide_comm(dd, O, name, p, spin=0, comm=True):
+    from distributed_ddpg_amd.learner import FusedLearner, init_comm
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    sess, actor, critic = _session(dd, O, name, p, batch_max=1024)
+    if comm:
+        init_comm(sess, 0, 1, single=True)
+    rb = ReplayBuffer(5000, 1234)
+    _fill(rb, S, A, 3000, scale, seed=2)
+    st = FusedLearner(sess, rb, 1024).step(stats=True)
+    out = _state(sess), st
+    sess.close()
+    return out
+
+
+@pytest.mark.parametrize("graph_comm", ["1", "0"])
+def test_comm_graph_matches_no_comm(dd, O, clean_env, graph_comm):
+    """A 1-rank communicator's exchange is an identity: with the step graph
+    capturing the RCCL calls (default) and eagerly (DDPG_GRAPH_COMM=0), one
+    fused step equals the communicator-less step bitwise (profiling off)."""
+    p, _ = _params(O, "wide")
+    ref = _wide_comm(dd, O, "wide", p, comm=False)
+    clean_env.setenv("DDPG_GRAPH_COMM", graph_comm)
+    got = _wide_comm(dd, O, "wide", p)
+    _same(got[0], ref[0])
+    assert got[1] == ref[1]
+
+
+@pytest.mark.parametrize("par,graph_comm", [("0", "1"), ("1", "1"), ("0", "0"), ("1", "0")])
+def test_comm_stream_ordering_spin(dd, O, clean_env, par, graph_comm):
+    """DDPG_TEST_CS_SPIN=300: on the comm stream, ahead of each collective
+    group, a kernel waits 300 us and then doubles the ranges the group
+    exchanges.  If Adam (or the slab reduction writing the tail ranges) were
+    not ordered behind the comm stream it would read undoubled gradients.
+    Checks, profiling off: the critic gradient buffer is exactly 2x the
+    no-spin run's and its Adam slots exactly 2x / 4x (fresh slots: m =
+    (1 - b1) g, v = (1 - b2) g^2 scale exactly by powers of two); for both
+    networks m == (1 - b1) G and v == (1 - b2) G^2 of the final buffer G, bitwise
+    with TF's formula (Adam consumed the doubled values)."""
+    p, _ = _params(O, "wide")
+    clean_env.setenv("DDPG_PAR", par)
+    clean_env.setenv("DDPG_GRAPH_COMM", graph_comm)
+    ref = _wide_comm(dd, O, "wide", p)
+    clean_env.setenv("DDPG_TEST_CS_SPIN", "300")
+    got = _wide_comm(dd, O, "wide", p)
+    state, ref_state = got[0], ref[0]
+    for g, g0 in zip(state[9], ref_state[9]):           # critic gradient
+        assert np.array_equal(g, 2 * g0)
+    for m, m0 in zip(state[6], ref_state[6]):
+        assert np.array_equal(m, 2 * m0)
+    for v, v0 in zip(state[7], ref_state[7]):
+        assert np.array_equal(v, 4 * v0)
+    one = np.float32(1)
+    c1, c2 = one - np.float32(0.9), one - np.float32(0.999)
+    for gi, mi, vi in ((9, 6, 7), (8, 4, 5)):
+        for g, m, v in zip(state[gi], state[mi], state[vi]):
+            g = g.astype(np.float32)
+            assert np.array_equal(m, (g - np.float32(0)) * c1)
+            assert np.array_equal(v, (g * g - np.float32(0)) * c2)

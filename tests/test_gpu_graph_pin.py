@@ -30,6 +30,10 @@ def O():
     return ddpg_oracle
 
 
+def _batch(z):
+    return z["step0/s"].shape[0]
+
+
 def _session(O, name):
     import torch
     assert torch.cuda.is_available()
@@ -40,7 +44,7 @@ def _session(O, name):
     actor = nets.ActorNetwork(S, A, scale, 1e-4, 1e-3, scaler, h1=H1, h2=H2)
     critic = nets.CriticNetwork(S, A, 1e-3, 1e-3, actor.get_num_trainable_vars(), scaler,
                                 h1=CH1, h2=CH2)
-    sess = nets.Session(batch_max=64)
+    sess = nets.Session(batch_max=_batch(z))
     actor.set_session(sess)
     critic.set_session(sess)
     sess.set_params(_lib.ACTOR, [p["actor"][k] for k in O.ACTOR_KEYS])
@@ -110,17 +114,31 @@ def _check_final(O, sess, z, fresh=False, lr=None):
         assert b2p == pytest.approx(float(z["final/beta2_power" + sfx]), rel=1e-6)
 
 
+@pytest.fixture
+def path_env(monkeypatch):
+    """B = 256 (ip1410_b256): the large-batch GEMM path (DDPG_SMALL=0) -- the
+    twin GEMMs with their in-launch K split, thin_k, skinny weight gradients and
+    slab reductions -- pinned to the executed graph directly."""
+    def set_for(name):
+        monkeypatch.delenv("DDPG_SMALL", raising=False)
+        if name == "ip1410_b256":
+            monkeypatch.setenv("DDPG_SMALL", "0")
+    return set_for
+
+
 @pytest.mark.parametrize("name", list(FIXTURES))
-def test_one_to_one_methods_follow_reference_graph(O, name):
+def test_one_to_one_methods_follow_reference_graph(O, name, path_env):
     from distributed_ddpg_amd import _lib
+    path_env(name)
     sess, actor, critic, z = _session(O, name)
+    B = _batch(z)
     for step in range(3):
         p = "step%d/" % step
         s, a, r, t, s2 = (z[p + k] for k in ("s", "a", "r", "t", "s2"))
         target_q = critic.predict_target(s2, actor.predict_target(s2))          # ddpg.py:90
         assert rel(target_q, z[p + "target_q"]) < FWD_TOL, step
         y = np.where(t[:, None], r[:, None], r[:, None] + 0.99 * target_q)     # ddpg.py:92-97
-        q, _, loss = critic.train(s, a, np.reshape(y, (64, 1)))                 # ddpg.py:100
+        q, _, loss = critic.train(s, a, np.reshape(y, (B, 1)))                  # ddpg.py:100
         assert rel(q, z[p + "q"]) < FWD_TOL, step
         assert abs(float(loss) - float(z[p + "loss"])) <= GRAD_TOL * float(z[p + "loss"])
         for n, g in zip(O.CKPT_CRITIC, sess.get_params(_lib.CRITIC_GRAD)):
@@ -139,24 +157,34 @@ def test_one_to_one_methods_follow_reference_graph(O, name):
 
 
 @pytest.mark.parametrize("name", list(FIXTURES))
-def test_fused_step_follows_reference_graph(O, name):
+def test_fused_step_follows_reference_graph(O, name, path_env):
     from distributed_ddpg_amd import _lib
-    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    path_env(name)
     sess, actor, critic, z = _session(O, name)
-    rb = ReplayBuffer(3 * 64, 1234)
+    B = _batch(z)
+    rb = ReplayBuffer(3 * B, 1234)
     for step in range(3):
         p = "step%d/" % step
         rb.add_batch(z[p + "s"], z[p + "a"], z[p + "r"], z[p + "t"], z[p + "s2"])
     assert rb.f64
-    fl = FusedLearner(sess, rb, 64)
+    fl = FusedLearner(sess, rb, B)
+    prof = Profile(sess)
     for step in range(3):
         p = "step%d/" % step
-        q_max, loss = fl.step_indices(np.arange(64 * step, 64 * (step + 1)), stats=True)
+        if step == 2 and B > 64:  # the last step profiled: which kernels ran
+            prof.enable(True)
+        q_max, loss = fl.step_indices(np.arange(B * step, B * (step + 1)), stats=True)
         assert abs(loss - float(z[p + "loss"])) <= GRAD_TOL * float(z[p + "loss"])
         assert q_max == pytest.approx(float(np.max(z[p + "q"])), rel=FWD_TOL)
         for which, names in ((_lib.CRITIC_GRAD, O.CKPT_CRITIC), (_lib.ACTOR_GRAD, O.CKPT_ACTOR)):
             for n, g in zip(names, sess.get_params(which)):
                 assert rel(g, z[p + "grad/" + n]) < GRAD_TOL, (step, n)
+    if B > 64:
+        keys = sorted(prof.read())
+        prof.enable(False)
+        assert any(k.startswith("gemm_h3_kernel") for k in keys), keys
+        assert not any(k.startswith("sb_") for k in keys), keys
     _check_final(O, sess, z, fresh=name.endswith("fresh"), lr=(1e-4, 1e-3))
     sess.close()

@@ -17,7 +17,9 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       (the default reads the EluGrad operand from the planes)
     DDPG_GEMM_H3=0    twin GEMMs with runtime ring-slot addressing (gemm_h_kernel,
                       gemm_h16_kernel) instead of gemm_h3_kernel / gemm_h16i_kernel
-                      (gemm_h3.h): same products, same order (fp32 and bf16)
+                      (gemm_h3.h): same products, same order (fp32 and bf16;
+                      both on the unsplit plan, DDPG_KCOMB=0, since only the
+                      gemm_h3.h kernels combine in-launch K splits)
     DDPG_TK_RPB=3     thin_k blocks walk 3 row tiles each (W panel staged once,
                       next X tile prefetched) instead of the automatic count
     DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
@@ -46,7 +48,8 @@ pytestmark = pytest.mark.gpu
 SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
-            "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO")
+            "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
+            "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN")
 
 
 @pytest.fixture(scope="module")
@@ -137,6 +140,10 @@ def _oracle(O, name, p, rows, steps):
 ])
 def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
+    if switch == "DDPG_GEMM_H3":
+        # gemm_h_kernel has no in-launch K split (small-M plan): compare both
+        # kernels on the same unsplit plan
+        monkeypatch.setenv("DDPG_KCOMB", "0")
     p, _ = _params(O, name)
     ref = _run(dd, O, name, p, 3)
     monkeypatch.setenv(switch, value)
@@ -165,6 +172,7 @@ def test_gemm_h3_switch_bf16_bitwise(dd, O, monkeypatch):
     gemm_h16_kernel with DDPG_GEMM_H3=0 -- same products in the same order,
     bitwise equal results after 2 fused steps."""
     _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_KCOMB", "0")  # gemm_h16_kernel has no in-launch K split
     p, _ = _params(O, "wide")
     ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
     assert any(k.startswith("gemm_h16i_kernel<RK,KR") for k in ref["keys"]), ref["keys"]

@@ -11,6 +11,8 @@ make_graph_fixtures.py / tfgraph.py):
                 0.999): Adam bias correction (networks.py:47,137 ApplyAdam's
                 beta1_power / beta2_power inputs and the Adam/Assign power
                 updates) is exercised -- step 1 applies alpha = 0.316 lr
+  ip1410_b256   the ip1410 start at the reference's default batch of 256
+                (parameters.py:11): on the GPU it runs the large-batch GEMM path
   mc120         the MountainCar graph (results/model_ddpg/model-120.meta: S=2,
                 actor 48/64, critic 48/128, the older networks.py whose actor
                 output is the tanh itself) from its own checkpoint (t ~ 45k),
@@ -40,6 +42,8 @@ FIXTURES = {
     "ip1410": ("graph_ip1410.npz", 4, 1, (128, 200), (128, 200), 3.0),
     "ip1410_fresh": ("graph_ip1410_fresh.npz", 4, 1, (128, 200), (128, 200), 3.0),
     "mc120": ("graph_mc120.npz", 2, 1, (48, 64), (48, 128), 1.0),
+    # the reference default batch (parameters.py:11): B = 256 rows per step
+    "ip1410_b256": ("graph_ip1410_b256.npz", 4, 1, (128, 200), (128, 200), 3.0),
 }
 
 
