@@ -1,0 +1,177 @@
+// Synchronous data parallelism (replacing the reference's TF
+// parameter server, ddpg.py:168-174): the RCCL exchange on the comm stream,
+// the stats all-gather, and the communicator ABI.  DESIGN.md §6.
+#include "ctx.h"
+
+// Data-parallel stats (world > 1): all[w] = rank w's {q_max, loss share};
+// max and an ordered sum, identical on every rank.
+__global__ void stats_reduce_kernel(const float* __restrict__ all, int world,
+                                    float* __restrict__ stats, double* __restrict__ acc) {
+  if (threadIdx.x != 0) return;
+  float qm = all[0], ls = all[1];
+  for (int w = 1; w < world; ++w) {
+    qm = fmaxf(qm, all[2 * w]);
+    ls = __fadd_rn(ls, all[2 * w + 1]);
+  }
+  stats[0] = qm;
+  stats[1] = ls;
+  if (acc) {
+    acc[0] += (double)qm;
+    acc[1] += (double)ls;
+    acc[2] += 1.0;
+  }
+}
+
+// Test hook of the data-parallel ordering (env DDPG_TEST_CS_SPIN=us; the
+// comm stream, ahead of a collective group): every block waits `us`
+// microseconds of wall clock (100 MHz s_memrealtime), then the grid doubles
+// the two gradient ranges the group exchanges (exact in fp32).  A reader not
+// ordered behind the comm stream would see the undoubled values.
+__global__ void cs_spin_scale_kernel(float* b0, long long n0, float* b1, long long n1, int us) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned long long)us)
+    __builtin_amdgcn_s_sleep(8);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long long i = i0; i < n0; i += stride) b0[i] = 2.f * b0[i];
+  for (long long i = i0; i < n1; i += stride) b1[i] = 2.f * b1[i];
+}
+
+
+static void nccl_try(ncclResult_t r) {
+  if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
+}
+
+// `to` waits for the work queued so far on `from` (comm-stream events cev)
+static void cs_link(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
+  if (from == to) return;
+  HIP_TRY(hipEventRecord(c->cev[ev], from));
+  HIP_TRY(hipStreamWaitEvent(to, c->cev[ev], 0));
+}
+
+// In-place RCCL sums of up to 2 disjoint ranges of the flat grad buffer, on
+// the comm stream after the work queued so far on c->cur (one group: one
+// launch).  The caller joins cs back before the gradients are read.
+// with_stats: the all-gather of the step's {q_max, loss} joins the same group
+// (one collective launch, one latency on the critical path instead of two);
+// stats_allreduce_on_cs then only reduces the gathered values.
+// window (profiling only): open an exchange-overlap record on the producing
+// stream, closed by the next join_cs -- the compute that stream runs between
+// issuing this exchange and waiting for it (bench.py's projected scaling).
+void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0,
+                            float* b1, size_t n1, bool with_stats,
+                            const char* window) {
+  if (!c->comm) return;
+  cs_link(c, ev, c->cur, c->cs);
+  const hipStream_t prev = c->cur;
+  if (window && c->prof && c->win_rec < 0) {
+    ProfRec rec{window, ev_get(c), ev_get(c), 0.0, (double)n0 * 4.0};
+    HIP_TRY(hipEventRecord(rec.e0, prev));
+    c->prof_recs.push_back(rec);
+    c->win_rec = (int)c->prof_recs.size() - 1;
+  }
+  c->cur = c->cs;
+  if (c->test_cs_spin) {
+    // test hook: the exchanged ranges doubled after a delay, on cs ahead of
+    // the group -- a consumer not ordered behind cs reads them undoubled
+    hipLaunchKernelGGL(cs_spin_scale_kernel, dim3(256), dim3(256), 0, c->cs, b0, (long long)n0,
+                       b1, (long long)n1, c->test_cs_spin);
+    HIP_TRY(hipGetLastError());
+  }
+  {
+    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0 + (with_stats ? 8.0 * c->cworld : 0.0));
+    nccl_try(ncclGroupStart());
+    if (n0) nccl_try(ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs));
+    if (n1) nccl_try(ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs));
+    if (with_stats)
+      nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
+    nccl_try(ncclGroupEnd());
+  }
+  c->cur = prev;
+}
+
+// the logged stats of a data-parallel step are the
+// global-batch ones (ddpg.py:102-103) -- max over ranks of max(Q) and the sum
+// of the ranks' loss shares (each already scaled by 1/B_global).  One
+// all-gather of every rank's {q_max, loss}, then an ordered reduction that
+// every rank computes identically; it also feeds the running sums.  On the
+// comm stream, after the critic all-reduce.
+void stats_allreduce_on_cs(ddpg_ctx* c, bool gathered) {
+  if (!c->comm) return;
+  const hipStream_t prev = c->cur;
+  c->cur = c->cs;
+  {
+    ProfScope ps(c, "rccl_stats", 0, gathered ? 0.0 : 8.0 * c->cworld);
+    if (!gathered)
+      nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(64), 0, c->cs, c->dstats_all, c->cworld,
+                       c->dstats, c->dacc);
+    HIP_TRY(hipGetLastError());
+  }
+  c->cur = prev;
+}
+
+// the consumer stream (c->cur) waits for every collective queued on cs
+void join_cs(ddpg_ctx* c, int ev) {
+  if (!c->comm) return;
+  if (c->win_rec >= 0) {  // close the exchange-overlap window on the consumer stream
+    HIP_TRY(hipEventRecord(c->prof_recs[c->win_rec].e1, c->cur));
+    c->win_rec = -1;
+  }
+  cs_link(c, ev, c->cs, c->cur);
+}
+
+extern "C" {
+
+// ---------------------------------------------------------------- comm
+// comm stream, its events and the stats all-gather buffer for a communicator
+// of `cworld` ranks
+static void comm_setup(ddpg_ctx* c, int cworld) {
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)cworld * sizeof(float)));
+  if (!c->cs) HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  for (auto& ev : c->cev)
+    if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+}
+
+int ddpg_comm_unique_id(char* out128) {
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    g_err = ncclGetErrorString(r);
+    return DDPG_ECOMM;
+  }
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  memcpy(out128, &id, 128);
+  return DDPG_OK;
+}
+
+int ddpg_comm_init(ddpg_ctx* c, const char* id128, int world, int rank) {
+  return guard(c, [&] {
+    if (world != c->world || rank != c->rank)
+      throw einval("comm (%d/%d) != cfg (%d/%d)", rank, world, c->rank, c->world);
+    if (!id128) throw einval("null unique id");
+    if (c->comm) throw DdpgError(DDPG_ESTATE, "communicator already initialised");
+    // world == 1 makes a 1-rank communicator: the data-parallel exchange then
+    // runs (as an identity) through the same RCCL call sites as world > 1
+    ncclUniqueId id;
+    memcpy(&id, id128, 128);
+    comm_setup(c, world);
+    nccl_try(ncclCommInitRank(&c->comm, world, id, rank));
+    c->cworld = world;
+  });
+}
+
+int ddpg_comm_init_proxy(ddpg_ctx* c) {
+  return guard(c, [&] {
+    if (c->comm) throw DdpgError(DDPG_ESTATE, "communicator already initialised");
+    ncclUniqueId id;
+    nccl_try(ncclGetUniqueId(&id));
+    comm_setup(c, 1);
+    nccl_try(ncclCommInitRank(&c->comm, 1, id, 0));
+    c->cworld = 1;
+  });
+}
+
+}  // extern "C"

@@ -30,59 +30,9 @@
 //                        layers: actor W3, critic Wo, critic Wa^T for dQ/da)
 #pragma once
 #include "common.h"
+#include "types.h"
 
 namespace ddpg {
-
-enum { L_RK = 0, L_KR = 1 };
-
-constexpr int GBK = 32, GNT = 256;
-constexpr int PROJ_MAX = 32;
-
-template <int BM, int BN>
-struct TileCfg {
-  static constexpr int STAGE = 2 * GBK * (BM + 1) + 2 * GBK * (BN + 1);
-  static constexpr int VS_LD = BN + 4;
-  static constexpr int EPI = (BM / 2) * VS_LD + BN * PROJ_MAX + 2 * GNT;  // red: up to 512 threads
-  static constexpr int SMEM = STAGE > EPI ? STAGE : EPI;
-};
-
-struct GemmEpi {
-  float* out;
-  long long out_split_stride;
-  int ldo;
-  int act;   // 0 none, 1 elu
-  int post;  // 0 none, 1 mul elu'(aux), 2 pw[n] * elu'(v)
-  int ldaux;
-  const float* bias;
-  const float* aux;
-  const float* pw;
-  float* colsum;  // [split * mtiles + mtile][ld_colsum]
-  int ld_colsum;
-  int proj_n, proj_sn, proj_sa;
-  const float* proj;  // Wp[n][a] = proj[n * proj_sn + a * proj_sa]
-  float* proj_out;    // [ntile][M][proj_n]
-  // bf16 twin of out (same element offsets, ld = ldo): h_planes = 1 stores
-  // bf16(v); 3 stores the exact h/m/l split of v, planes h_plane_stride apart.
-  // Read by the bf16-operand GEMM (gemm_h.h).  Needs N, ldo % 4 == 0.
-  __bf16* outh;
-  long long h_plane_stride;
-  int h_planes;
-  // post 1 with auxh (and aux == nullptr): the EluGrad operand is read from
-  // its three exact bf16 planes ((h + m) + l == the fp32 value), offsets and
-  // ld as aux, planes auxh_ps apart -- for activations whose fp32 copy is not
-  // written (fp32 contexts whose other readers all take the twin)
-  const __bf16* auxh;
-  long long auxh_ps;
-};
-
-struct GemmArgs {
-  const float* A;
-  const float* B;
-  int M, N, K, lda, ldb;
-  int kps;  // k extent per split (multiple of GBK)
-  int xcd;  // 1: XCD-aware tile order (xcd_tile)
-  GemmEpi e;
-};
 
 // XCD-aware tile order (guide T1, bijective form): hardware deals workgroups
 // round-robin over the 8 XCDs, so consecutive linear ids land on different

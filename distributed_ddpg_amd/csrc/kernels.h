@@ -81,56 +81,6 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
   }
 }
 
-// Row gather of one ring plane as raw 32-bit words (host sample_batch path:
-// the rows keep the ring's precision; row_bytes is a multiple of 4).
-__global__ void gather_bytes_kernel(const int* __restrict__ slots, int B,
-                                    const unsigned char* __restrict__ src,
-                                    unsigned char* __restrict__ dst, long long row_bytes) {
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const long long words = row_bytes >> 2;
-  for (int b = wave; b < B; b += nwaves) {
-    const unsigned* ps = (const unsigned*)(src + (size_t)slots[b] * row_bytes);
-    unsigned* pd = (unsigned*)(dst + (size_t)b * row_bytes);
-    for (long long j = lane; j < words; j += 64) pd[j] = ps[j];
-  }
-}
-
-// Data-parallel stats (world > 1): all[w] = rank w's {q_max, loss share};
-// max and an ordered sum, identical on every rank.
-__global__ void stats_reduce_kernel(const float* __restrict__ all, int world,
-                                    float* __restrict__ stats, double* __restrict__ acc) {
-  if (threadIdx.x != 0) return;
-  float qm = all[0], ls = all[1];
-  for (int w = 1; w < world; ++w) {
-    qm = fmaxf(qm, all[2 * w]);
-    ls = __fadd_rn(ls, all[2 * w + 1]);
-  }
-  stats[0] = qm;
-  stats[1] = ls;
-  if (acc) {
-    acc[0] += (double)qm;
-    acc[1] += (double)ls;
-    acc[2] += 1.0;
-  }
-}
-
-// Test hook of the data-parallel ordering (env DDPG_TEST_CS_SPIN=us; the
-// comm stream, ahead of a collective group): every block waits `us`
-// microseconds of wall clock (100 MHz s_memrealtime), then the grid doubles
-// the two gradient ranges the group exchanges (exact in fp32).  A reader not
-// ordered behind the comm stream would see the undoubled values.
-__global__ void cs_spin_scale_kernel(float* b0, long long n0, float* b1, long long n1, int us) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * (unsigned long long)us)
-    __builtin_amdgcn_s_sleep(8);
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (long long i = i0; i < n0; i += stride) b0[i] = 2.f * b0[i];
-  for (long long i = i0; i < n1; i += stride) b1[i] = 2.f * b1[i];
-}
-
 // ---------------------------------------------------------------- thin heads
 // actor output: o = tanh(sum_t part[t][b][a]); mu = o * scale  (networks.py:59-61)
 __global__ void actor_out_kernel(const float* __restrict__ part, int NT, int B, int A,

@@ -37,6 +37,7 @@
 // ApplyAdam, soft update); only the summation order differs.
 #pragma once
 #include "common.h"
+#include "types.h"
 
 namespace ddpg {
 
@@ -64,18 +65,7 @@ constexpr int SB_GT = 256;     // threads of the weight-gradient / Adam kernel
 typedef __attribute__((address_space(1))) f32x4 glb_v4;
 typedef __attribute__((address_space(3))) f32x4 lds_v4;
 
-// Saved per-row tensors that the weight gradients read, feature-major
-// ([feature][Bp], Bp = Bmax rounded up to 4): a workgroup stores its 4 rows of
-// a feature as one float4 and the gradient kernel reads a feature's batch
-// column as contiguous float4s.
-struct SbSave {
-  int Bp;
-  float *xs, *xa;          // [S], [A]      inputs (scaled)
-  float *cat, *dcat;       // [2 CH1]       critic concat, its gradient
-  float *h, *dhp, *dq;     // [CH2],[CH2],[1] critic hidden, its pre-act grad, dQ
-  float *h1, *h2;          // [AH1], [AH2]  actor hidden
-  float *dz1, *dz2, *dz3;  // [AH1], [AH2], [A]
-};
+
 
 // Per-step arguments (device pointers; offsets into the flat layout).
 struct SbArgs {
@@ -640,27 +630,7 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
   }
 }
 
-// One network's weight-gradient table: tensor i occupies param offsets
-// [off, off + K*N) (row-major [K][N]); its gradient is
-//   g[k][n] = sum_b X[k][b] dY[n][b]   (feature-major saves; X == nullptr: bias, X = 1)
-// over the B saved rows, computed by tiles of TK x TN elements (TK*TN = SB_GT)
-// starting at block tile0.
-struct SbGradT {
-  long long off;
-  int K, N;
-  const float* X;
-  int ldx;
-  const float* dY;
-  int ldy;
-  int TN, TK, tile0;
-};
-constexpr int SB_MAXT = 10;  // tensors per network + the sentinel
-struct SbGradTab {
-  SbGradT t[SB_MAXT];
-  int n;
-  int shadow;  // index of the tensor whose transpose is kept (Wh / W2), -1 none
-  float* sh;
-};
+
 
 // Weight gradients of one network over the whole batch (one ordered fp32
 // sum over b per element, no partial slabs), TF ApplyAdam with this step's

@@ -20,6 +20,7 @@
 // critic state and action branches).
 #pragma once
 #include "common.h"
+#include "types.h"
 
 // Phase timestamp hook for tools/thin_k_bench.hip; empty in the product build.
 #ifndef TK_STAMP
@@ -28,58 +29,6 @@
 
 namespace ddpg {
 
-constexpr int TK_MAXK = 64;
-#ifndef TK_COLS_CFG
-#define TK_COLS_CFG 128
-#endif
-constexpr int TK_ROWS = 64, TK_COLS = TK_COLS_CFG, TK_NT = 256;
-static_assert(TK_COLS == 64 || TK_COLS == 128, "thin_k column block");
-constexpr int TK_TPW = TK_COLS / 64;       // 32x32 tiles per wave (4 waves: 2 x 2)
-constexpr int TK_KQS = TK_NT / TK_COLS;    // k-quad stride of the W panel loads
-constexpr int TK_WJ = 16 / TK_KQS;         // W panel float4 loads per thread
-constexpr int TK_OCT = TK_COLS / 8;        // column octets of the epilogue
-constexpr int TK_RG = TK_NT / TK_OCT;      // epilogue row groups
-constexpr int TK_KALIGN = 8;
-
-struct TkPart {
-  const float* X;   // [M][ldx], 16-byte aligned, ldx % 4 == 0
-  int ldx, K;       // K % 8 == 0
-  const float* W;   // w_nk ? W[n][k] (ldw) : W[k][n] (ldw); 16-byte aligned, ldw % 4 == 0
-  int ldw, w_nk;
-  int N;              // N % 4 == 0
-  const float* bias;  // [N] or null
-  int act;            // 1: elu
-  const float* aux;   // v *= EluGrad factor of aux[m][n] (ldaux), or null
-  int ldaux;
-  float* out;         // out[m * ldo + n]
-  int ldo;
-  __bf16* outh;       // bf16 twin of out (same offsets; hnp planes, hps apart), or null
-  long long hps;
-  int hnp;
-  float* colsum;      // [row block][ld_colsum] partial column sums of v, or null
-  int ld_colsum;
-};
-
-constexpr int TK_MAXP = 5;  // parts per launch (blockIdx.z)
-
-struct TkArgs {
-  TkPart p[TK_MAXP];
-  int M;
-  int mt;   // row tiles (ceil(M / TK_ROWS))
-  int rpb;  // row tiles per block (blockIdx.y owns [rpb * y, rpb * y + rpb))
-};
-
-// LDS: the W image (3 planes, resident for the whole block), then one region
-// shared by the X image (3 planes) of the current row tile and, after its
-// MFMAs, the raw output tile [64 rows][TK_COLS] (16-B chunks XOR-swizzled by
-// row: tk_oidx), then the column-sum scratch of the epilogue.
-constexpr int TK_XIMG = TK_ROWS * 128;  // bytes per X plane
-constexpr int TK_WIMG = TK_COLS * 128;  // bytes per W plane
-constexpr int TK_OUT_BYTES = TK_ROWS * TK_COLS * 4;
-constexpr int TK_XREG = 3 * TK_XIMG > TK_OUT_BYTES ? 3 * TK_XIMG : TK_OUT_BYTES;
-constexpr int TK_LDS = 3 * TK_WIMG + TK_XREG;
-static_assert(TK_LDS <= 80 * 1024, "two blocks per CU");
-static_assert(TK_RG * TK_COLS * 4 <= TK_XREG, "column-sum scratch aliases the output tile");
 // Three-plane bf16 images (the exact split x = h + m + l of every fp32
 // operand, as the twins of gemm_h.h): [plane][row][64 k] with 128-B rows, 16-B
 // chunk c of row r at c ^ ((r >> 1) & 7) -- every 32x32x16 fragment read

@@ -156,9 +156,10 @@ def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
     default 16x16x32 kernel -- bitwise -- and against the oracle at the stated
     bf16 bar."""
     _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_KCOMB", "0")  # gemm_h_kernel has no in-launch K split
     p, _ = _params(O, "wide")
     ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
-    assert any(k.startswith("gemm_h16_kernel") for k in ref["keys"]), ref["keys"]
+    assert any(k.startswith("gemm_h16") for k in ref["keys"]), ref["keys"]
     monkeypatch.setenv("DDPG_GEMM_MF", "32")
     got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
     assert any(k.startswith("gemm_h_kernel") and "NP=1" in k for k in got["keys"]), got["keys"]
@@ -322,3 +323,39 @@ def test_gradient_sets_are_get_only(dd, O):
         with pytest.raises(RuntimeError, match="get-only"):
             sess.set_params(which, g)
     sess.close()
+
+
+@pytest.mark.parametrize("name", ["ip", "wide"])
+def test_slots_in_place_ring_reuse_pipelined(dd, O, monkeypatch, name):
+    """The step's replay slots are read in place from pinned (coherent) host
+    memory: a ring of kSlotRing = 4 buffers, each rewritten by the host four
+    steps later once its event has fired.  Ten eager steps (DDPG_GRAPH=0)
+    issued back to back without a host sync -- a pipelined caller, so the ring
+    wraps while earlier steps may still run -- equal the uploaded-slots path
+    (DDPG_SLOTS_H2D=1) bitwise.  ip: the small-batch path; wide: large batch."""
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_GRAPH", "0")
+    p, _ = _params(O, name)
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+
+    def run():
+        sess, actor, critic = _session(dd, O, name, p)
+        rb = ReplayBuffer(5000, 1234)
+        _fill(rb, S, A, 3000, scale, seed=4)
+        fl = FusedLearner(sess, rb, B)
+        for _ in range(10):
+            fl.step()
+        sess.sync()
+        out = ([sess.get_params(w) for w in (0, 2, 8, 9)], fl.read_stats())
+        sess.close()
+        return out
+
+    got = run()
+    monkeypatch.setenv("DDPG_SLOTS_H2D", "1")
+    ref = run()
+    assert got[1] == ref[1]
+    for x, y in zip(got[0], ref[0]):
+        for u, v in zip(x, y):
+            assert np.array_equal(u, v)

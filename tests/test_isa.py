@@ -36,14 +36,13 @@ def test_library_has_no_scratch_and_no_async_return_hazards(isa):
 
 
 def test_every_gemm_and_thin_k_kernel_is_covered(isa):
-    co = isa.code_object(SO)
-    res = isa.kernel_resources(co)
+    res = isa.kernel_resources_all(SO)  # every translation unit's code object
     names = list(res)
     assert any("gemm_h_kernel" in n for n in names)
     assert any("gemm_h16_kernel" in n for n in names)
     assert any("thin_k_kernel" in n for n in names)
     assert any("gemm_h256_kernel" in n for n in names)
-    dis = isa.disassemble(co)
+    dis = isa.disassemble_all(SO)
     for n in names:
         if re.search(isa.EPILOGUE_SPILL_OK, n):
             # allowed epilogue spills only: no scratch load inside the MFMA main loop

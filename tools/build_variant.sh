@@ -9,5 +9,5 @@ mkdir -p "$ROOT/build_variants"
 V=$1
 shift
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall \
-  -Wno-unused-function -I/opt/rocm/include "$@" ddpg_api.hip sampler.cpp crc32c.cpp -shared \
+  -Wno-unused-function -I/opt/rocm/include "$@" gemm.hip step.hip dp.hip replay.hip abi.hip sampler.cpp crc32c.cpp -shared \
   -L/opt/rocm/lib -lrccl -Wl,-soname,libddpg_hip.so -o "$ROOT/build_variants/lib_$V.so"

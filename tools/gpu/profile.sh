@@ -10,7 +10,7 @@ CFG=${1:-c3}; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$CFG
 rm -rf $OUT; mkdir -p $OUT
-ARGS="--config $CFG --no-cpu --no-small --steps 20 --warmup 5 --profile-steps 20 $*"
+ARGS="--config $CFG --no-cpu --no-small --no-project --steps 20 --warmup 5 --profile-steps 20 $*"
 # fused steps per run: warmup + steps + latency pass (20) + profile pass (20)
 NSTEPS=65
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py $ARGS \

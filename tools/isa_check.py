@@ -45,8 +45,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEFAULT_SO = os.path.join(ROOT, "distributed_ddpg_amd", "libddpg_hip.so")
 
 
-def code_object(so_path, arch="gfx950"):
-    """The `arch` code object of the library's .hip_fatbin offload bundle."""
+def code_objects(so_path, arch="gfx950"):
+    """Every `arch` code object of the library's .hip_fatbin section: one clang
+    offload bundle per translation unit, concatenated (aligned)."""
     out = "/tmp/isa_check_%d.fatbin" % os.getpid()
     copy = out + ".so"  # objcopy writes a copy of its input; discarded
     subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", ".hip_fatbin=" + out,
@@ -60,16 +61,45 @@ def code_object(so_path, arch="gfx950"):
     magic = b"__CLANG_OFFLOAD_BUNDLE__"
     if not data.startswith(magic):
         raise ValueError("no clang offload bundle in %s" % so_path)
-    (n,) = struct.unpack_from("<Q", data, len(magic))
-    o = len(magic) + 8
-    for _ in range(n):
-        off, size, tlen = struct.unpack_from("<QQQ", data, o)
-        o += 24
-        triple = data[o:o + tlen].decode()
-        o += tlen
-        if triple.endswith(arch):
-            return data[off:off + size]
-    raise ValueError("no %s code object in %s" % (arch, so_path))
+    cos = []
+    start = 0
+    while start >= 0:
+        (n,) = struct.unpack_from("<Q", data, start + len(magic))
+        o = start + len(magic) + 8
+        end = start
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, o)
+            o += 24
+            triple = data[o:o + tlen].decode()
+            o += tlen
+            end = max(end, start + off + size)
+            if triple.endswith(arch) and size:
+                cos.append(data[start + off:start + off + size])
+        start = data.find(magic, max(end, start + 1))
+    if not cos:
+        raise ValueError("no %s code object in %s" % (arch, so_path))
+    return cos
+
+
+def code_object(so_path, arch="gfx950"):
+    """The first `arch` code object (single-unit libraries)."""
+    return code_objects(so_path, arch)[0]
+
+
+def kernel_resources_all(so_path):
+    """kernel_resources merged over every code object of the library."""
+    out = {}
+    for co in code_objects(so_path):
+        out.update(kernel_resources(co))
+    return out
+
+
+def disassemble_all(so_path):
+    """disassemble merged over every code object of the library."""
+    out = {}
+    for co in code_objects(so_path):
+        out.update(disassemble(co))
+    return out
 
 
 def _run(tool, co, *args):
@@ -308,12 +338,11 @@ def _scratch_in_main_loop(insns):
 
 def check(so_path=DEFAULT_SO, kernels_like=None, verbose=False):
     """Returns a list of problem strings (empty: the library passes)."""
-    co = code_object(so_path)
     problems = []
-    res = kernel_resources(co)
+    res = kernel_resources_all(so_path)
     if not res:
         problems.append("no kernel metadata found")
-    dis = disassemble(co)
+    dis = disassemble_all(so_path)
     for k, r in sorted(res.items()):
         # (SGPR spills go to VGPR lanes with v_writelane: synchronous, no scratch)
         if r.get("scratch", 0) or r.get("vgpr_spill", 0):
