@@ -109,6 +109,21 @@ def spawn_ranks(n):
     return rc if rc >= 0 else 128 - rc
 
 
+class stdout_to_stderr:
+    """Point fd 1 at stderr for the duration (native libraries' banners), so
+    that stdout carries only the one JSON line of the bench contract."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="fp32",
                   per_gpu_b=None, rb=None, proxy=False):
     """Session + replay ring (filled, or `rb` reused) + fused learner.
@@ -129,10 +144,11 @@ def build_learner(cfg_name, device, rank, world, replay_rows, seed=1234, dtype="
     sess.run(nets.global_variables_initializer(seed=seed))   # same init on every rank
     actor.update_target_network()                            # ddpg.py:228-229
     critic.update_target_network()
-    if proxy:
-        _lib.check(_lib.lib.ddpg_comm_init_proxy(sess.ctx), sess.ctx)
-    else:
-        init_comm(sess, rank, world)
+    with stdout_to_stderr():   # RCCL prints a version banner on fd 1 at init
+        if proxy:
+            _lib.check(_lib.lib.ddpg_comm_init_proxy(sess.ctx), sess.ctx)
+        else:
+            init_comm(sess, rank, world)
     if rb is None:
         rb = ReplayBuffer(replay_rows, seed, device=device)
         t0 = time.time()
@@ -198,9 +214,13 @@ def per_rank_step(cfg_name, device, n, mode, rb, dtype, steps=30, warmup=5, prof
     win = {k.split("|", 1)[1]: 1e3 * v["ms"] / v["launches"] for k, v in rows.items()
            if k.startswith("xwin|")}
     busy = sum(v["ms"] for k, v in rows.items() if not k.startswith(("rccl", "xwin"))) / prof_steps
+    by_kernel = summarize_profile(rows, prof_steps)[0]
+    top = sorted(((k, v) for k, v in by_kernel.items() if not k.startswith("xwin")),
+                 key=lambda kv: -kv[1]["ms"])[:8]
     return {"per_rank_batch": b, "step_ms": round(1000.0 * el / steps, 4),
             "gpu_busy_ms": round(busy, 4),
-            "window_us": {k: round(v, 1) for k, v in win.items()}}
+            "window_us": {k: round(v, 1) for k, v in win.items()},
+            "kernels_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in top}}
 
 
 def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):

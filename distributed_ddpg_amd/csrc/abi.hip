@@ -167,6 +167,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.kcomb = !env_is("DDPG_KCOMB", "0");
       if (const char* v = getenv("DDPG_KCOMB_BLOCKS"))
         c->sw.kc_blocks = std::min(kKcTickets, std::max(1, atoi(v)));
+      if (const char* v = getenv("DDPG_KCOMB_SPLITS"))
+        c->sw.kc_splits = std::min(KC_MAXS, std::max(2, atoi(v)));
       if (const char* v = getenv("DDPG_TEST_CS_SPIN")) c->test_cs_spin = std::max(0, atoi(v));
       if (env_is("DDPG_GRAPH_COMM", "0")) c->comm_graph = false;
     }

@@ -270,7 +270,7 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       if (splits_req == 1 && kc_kernel && c->kc_part) {
         const int tiles = h.nt(N) * h.mt(M);
         const int nkt = Kh / BKh;
-        int sk = std::min(ceil_div(256, tiles), nkt / 3);
+        int sk = std::min({ceil_div(256, tiles), nkt / 3, c->sw.kc_splits});
         if (tiles < c->sw.kc_blocks && sk >= 2) {
           const int kps = ceil_div(nkt, sk) * BKh;
           sk = ceil_div(Kh, kps);

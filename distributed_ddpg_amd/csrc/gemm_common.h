@@ -361,58 +361,97 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
 // 0 .. S-1 (its own from registers), so the sum does not depend on which
 // split arrives last (bitwise reproducible), resets the ticket for the next
 // launch and returns true; the other blocks return false and exit.
-// Visibility across XCDs (each has its own L2): agent-scope release before
-// the ticket (the partial stores written back), acquire after it.
+// Cross-XCD hand-off without cache flushes (MI355X_MICROARCH.md, the sc1
+// hand-off table, first row): the partials are stored and loaded with sc1
+// (16 B per lane, lane-linear so that one wave instruction covers 1 KiB of
+// whole lines -- a 64-B lane stride made every instruction a 64-line partial
+// write and tripled the hand-off, 7-10 -> 2-3 us; written through past the
+// storing XCD's L2, read past the reading CU's caches), every storing wave waits vmcnt(0) before the
+// workgroup barrier, then ONE lane's agent-scope atomic add on the tile's
+// counter; the block whose add returns S - 1 loads after a barrier.  (An
+// agent fence per wave instead -- buffer_wbl2 + buffer_inv -- cost more than
+// the split saved.)  The sc1 accesses are the buffer intrinsics with cache
+// policy 16 (sc1), which the compiler sees, so it orders and waits for them
+// and keeps the store-data hazards (an inline-asm store whose data registers
+// were rewritten one cycle later gave run-to-run differences).
+constexpr int KC_SC1 = 16;  // CPol SC1
+
 template <int NV>
 DDPG_DEV bool ksplit_combine(f32x16* acc, float* part, unsigned* ticket, int tile, int z, int S,
                              int tid, int nt) {
   __shared__ unsigned last_s;
-  const size_t slab = (size_t)NV * nt * 16;
-  float* base = part + (size_t)tile * S * slab;
-  {
-    float* mine = base + (size_t)z * slab;
+  const unsigned slab = (unsigned)(NV * nt * 16 * 4);  // bytes per (tile, split)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(part + (size_t)tile * S * (slab / 4)), 0, 0x7fffffff, 0x00020000);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      float4* o = reinterpret_cast<float4*>(mine + ((size_t)v * nt + tid) * 16);
+  for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        o[q] = make_float4(acc[v][4 * q], acc[v][4 * q + 1], acc[v][4 * q + 2], acc[v][4 * q + 3]);
-    }
-  }
-  __threadfence();  // release: this thread's partial is visible device-wide
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, f32x4{acc[v][4 * q], acc[v][4 * q + 1], acc[v][4 * q + 2],
+                                          acc[v][4 * q + 3]}),
+          rs, z * slab + (unsigned)(((v * 4 + q) * nt + tid) * 16), 0, KC_SC1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has left
   __syncthreads();
   if (tid == 0) {
     const unsigned old =
-        __hip_atomic_fetch_add(ticket + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ticket + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned l = old == (unsigned)(S - 1);
     if (l) __hip_atomic_store(ticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_s = l;
   }
   __syncthreads();
   if (!last_s) return false;
-  __threadfence();  // acquire: the other splits' partials
-  f32x16 own[NV];
+  auto ld = [&](int zz, int v, int q) {
+    return __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                   rs, zz * slab + (unsigned)(((v * 4 + q) * nt + tid) * 16), 0, KC_SC1));
+  };
+  if constexpr (NV <= 2) {
+    // every other split's partial in flight at once (one memory round trip,
+    // not S - 1 of them): slot j holds split j + (j >= z); then the sum in
+    // split order 0 .. S-1 (the host caps S at KC_MAXS)
+    f32x4 x[KC_MAXS - 1][NV][4];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) own[v] = acc[v];
-  for (int zz = 0; zz < S; ++zz) {
-    const float* src = base + (size_t)zz * slab;
+    for (int j = 0; j < KC_MAXS - 1; ++j) {
+      const int zz = j + (j >= z);
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x16 p;
-      if (zz == z) {
-        p = own[v];
-      } else {
-        const float4* s4 = reinterpret_cast<const float4*>(src + ((size_t)v * nt + tid) * 16);
+      for (int v = 0; v < NV; ++v)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 x = s4[q];
-          p[4 * q] = x.x;
-          p[4 * q + 1] = x.y;
-          p[4 * q + 2] = x.z;
-          p[4 * q + 3] = x.w;
-        }
+        for (int q = 0; q < 4; ++q) x[j][v][q] = zz < S ? ld(zz, v, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 own{acc[v][4 * q], acc[v][4 * q + 1], acc[v][4 * q + 2], acc[v][4 * q + 3]};
+        f32x4 t = z == 0 ? own : x[0][v][q];
+#pragma unroll
+        for (int zz = 1; zz < KC_MAXS; ++zz)
+          if (zz < S) t += zz == z ? own : zz < z ? x[zz][v][q] : x[zz - 1][v][q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[v][4 * q + e] = t[e];
       }
-      acc[v] = zz == 0 ? p : acc[v] + p;
+  } else {
+    // 256-row tiles (64 accumulators per lane): no registers for S - 1
+    // partials at once -- one split per round trip, in split order
+    f32x16 own[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) own[v] = acc[v];
+    for (int zz = 0; zz < S; ++zz) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        f32x16 p = own[v];
+        if (zz != z)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 y = ld(zz, v, q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) p[4 * q + e] = y[e];
+          }
+        acc[v] = zz == 0 ? p : acc[v] + p;
+      }
     }
   }
   return true;

@@ -52,6 +52,9 @@ struct GemmHArgs {
   // are separate slabs (weight gradients) or there is one split
   float* kpart = nullptr;
   unsigned* kticket = nullptr;
+#ifdef DDPG_KC_STAMPS
+  unsigned long long* stamps = nullptr;  // tools/kc_bench.hip only: per-block phase clocks
+#endif
 };
 
 constexpr int HG_NT = 512, HG_BN = 128, HG_STAGES = 3;

@@ -30,7 +30,16 @@
 namespace ddpg {
 
 template <int AL, int BL>
+#ifdef DDPG_KC_STAMPS  // tools/kc_bench.hip: s_memrealtime per phase, lane 0 of each block
+#define KC_STAMP(i)                                                                    \
+  if (g.stamps && threadIdx.x == 0)                                                    \
+    g.stamps[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (i)] = \
+        __builtin_amdgcn_s_memrealtime();
+#else
+#define KC_STAMP(i)
+#endif
 __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
+  KC_STAMP(0)
   constexpr int NP = 3, BM = 128, BK = 32, WGN = 4;
   using C = HgCfg<BM, BK, NP, 8>;
   constexpr int TM = BM / 64;  // 2 32-row A fragments per wave
@@ -267,6 +276,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) acc[i][0] += acs[i][0];
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  KC_STAMP(1)
   int ze = z;
   if (g.kpart) {  // small-M plan: this launch's splits are combined here
     if (!ksplit_combine<TM>(&acc[0][0], g.kpart, g.kticket, by * gridDim.x + bx, z, gridDim.z,
@@ -274,12 +284,14 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
       return;
     ze = 0;
   }
+  KC_STAMP(2)
   __syncthreads();  // staging buffers are reused by the epilogue
   GemmArgs ge;
   ge.M = g.M;
   ge.N = g.N;
   ge.e = g.e;
   gemm_epilogue<BM, HG_BN, WGN>(acc, smem, ge, tid, n0, m0, ze, bx, by);
+  KC_STAMP(3)
 }
 
 }  // namespace ddpg

@@ -11,6 +11,9 @@ namespace ddpg {
 // ---------------------------------------------------------------- GEMMs (gemm_common.h)
 enum { L_RK = 0, L_KR = 1 };
 
+// in-launch K split (ksplit_combine, gemm_common.h): at most KC_MAXS splits
+// per tile -- the partials the last block holds in registers at once
+constexpr int KC_MAXS = 4;
 constexpr int GBK = 32, GNT = 256;
 constexpr int PROJ_MAX = 32;
 

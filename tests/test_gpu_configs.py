@@ -237,6 +237,14 @@ BF16_FWD_TOL, BF16_DA_TOL, BF16_GRAD_NORM_TOL, BF16_PARAM_TOL = 2e-2, 5e-2, 3e-2
 # Adam first-moment slot after the first step, m = (1 - beta1) g: max-rel bar
 # (max |m - 0.1 g_ref| / max |0.1 g_ref|) against the float64 oracle gradient
 BF16_M_MAXREL = 5e-2
+# per-tensor max-rel gradient bar beside the norm-wise one: max |g - g_ref| /
+# max |g_ref| over each tensor, so one bad row of a 2048-wide layer fails it
+BF16_GRAD_MAXREL = 5e-2
+
+
+def maxrel(x, r):
+    x, r = np.asarray(x, np.float64), np.asarray(r, np.float64).reshape(np.shape(x))
+    return float(np.max(np.abs(x - r)) / max(np.max(np.abs(r)), 1e-30))
 
 
 def test_c5_bf16_full_dims(dd, O):
@@ -278,6 +286,7 @@ def test_c5_bf16_full_dims(dd, O):
                            (_lib.ACTOR_GRAD, out["actor_grads"], O.ACTOR_KEYS)):
         for k, g in zip(keys_, sess.get_params(gw)):
             assert normrel(g, ref[k]) < BF16_GRAD_NORM_TOL, ("grad", k, normrel(g, ref[k]))
+            assert maxrel(g, ref[k]) < BF16_GRAD_MAXREL, ("grad max-rel", k, maxrel(g, ref[k]))
     # Adam slots after the first step (fresh state): m = (1 - beta1) g and
     # v = (1 - beta2) g^2 of the GPU's own gradient, and m against the
     # oracle's gradient at the stated bf16 max-rel bar

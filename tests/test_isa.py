@@ -83,3 +83,17 @@ def test_hazard_scan_catches_async_return_clobber(isa):
           (0x10, "s_endpgm", "", None)]
     hz = isa.scan_kernel(ok)
     assert [a for a, *_ in hz] == [0xc]
+
+
+def test_store_data_hazard_detected(isa):
+    """A 16-B store whose data registers the next VALU instruction rewrites
+    (an inline-asm store hipcc does not pad) is reported; with a wait state
+    between, it is not."""
+    bad = [(0x0, "global_store_dwordx4", "v[0:1], v[4:7], off sc1", None),
+           (0x8, "v_mov_b32_e32", "v5, 0", None), (0xc, "s_endpgm", "", None)]
+    assert [a for a, *_ in isa.store_data_hazards(bad)] == [0x0]
+    ok = [bad[0], (0x8, "s_nop", "0", None), bad[1], bad[2]]
+    assert isa.store_data_hazards(ok) == []
+    buf = [(0x0, "buffer_store_dwordx4", "v[4:7], v8, s[0:3], 0 offen sc1", None),
+           (0x8, "v_add_f32_e32", "v6, v1, v2", None)]
+    assert [a for a, *_ in isa.store_data_hazards(buf)] == [0x0]

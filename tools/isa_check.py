@@ -260,6 +260,26 @@ def _step(state, mn, ops, report=None):
     return (lds[-15:], vm[-63:], fl[-15:])
 
 
+def store_data_hazards(insns):
+    """VMEM stores of more than 8 bytes read their data VGPRs after issue: a
+    VALU write of those registers in the next instruction (no wait state
+    between) corrupts the stored value.  hipcc inserts the wait for its own
+    stores but not after an inline-asm store (the round-4 split-K partial
+    stores showed it as run-to-run differences).  [(addr, store, writer)]"""
+    out = []
+    wide = ("dwordx3", "dwordx4", "_b96", "_b128")
+    for i, (a, mn, ops, _) in enumerate(insns[:-1]):
+        if not (mn.startswith(("global_store", "buffer_store", "flat_store", "scratch_store")) and
+                mn.endswith(wide)):
+            continue
+        parts = [x.strip() for x in ops.split(",")]
+        data = _regs(parts[0] if mn.startswith("buffer_") else (parts[1] if len(parts) > 1 else ""))
+        _, nmn, nops, _ = insns[i + 1]
+        if nmn.startswith("v_") and nops and _regs(nops.split(",")[0]) & data:
+            out.append((a, "%s %s" % (mn, ops), "%s %s" % (nmn, nops)))
+    return out
+
+
 def scan_kernel(insns):
     """Async-return hazards of one kernel: [(addr, insn text, queue, regs)]."""
     if not insns:
@@ -353,6 +373,9 @@ def check(so_path=DEFAULT_SO, kernels_like=None, verbose=False):
     for k, insns in sorted(dis.items()):
         if kernels_like and not re.search(kernels_like, k):
             continue
+        for a, st, wr in store_data_hazards(insns)[:5]:
+            problems.append("%s +0x%x: %s has its data registers rewritten by %s with no wait state"
+                            % (k, a - insns[0][0], st, wr))
         hz = scan_kernel(insns)
         for a, txt, q, r in hz[:5]:
             problems.append("%s +0x%x: %s touches %s registers %s still being written"
