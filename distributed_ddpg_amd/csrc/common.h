@@ -9,7 +9,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define DDPG_DEV __device__ __forceinline__
 
 // TF 1.3 Elu: (x < 0).select(exp(x) - 1, x)
-DDPG_DEV float elu_f(float x) { return x < 0.f ? __fsub_rn(expf(x), 1.f) : x; }
+// elu: exp(x) - 1 for x < 0 (TF 1.3's Elu, exp then subtract) with exp(x) as
+// 2^(x log2 e) on v_exp_f32 (1 ulp).  Rounding x log2 e moves exp(x) by at
+// most |x| 2^-24 ln 2 relative, so the absolute error of elu stays below
+// ~1.5e-7 for every x < 0 -- within the fp32 subtraction's own rounding of
+// the libm form, at 3 instructions instead of ~12 (the epilogues that apply it
+// are VALU-bound: thin_k's five-part launch 49.5 -> 44.2 us,
+// profiles/r4/thin_k_fast_elu.txt)
+DDPG_DEV float elu_f(float x) {
+  return x < 0.f ? __fsub_rn(__builtin_amdgcn_exp2f(__fmul_rn(x, 1.44269504f)), 1.f) : x;
+}
 // TF 1.3 EluGrad from the OUTPUT y: y < 0 ? dy * (y + 1) : dy
 DDPG_DEV float elu_grad_factor(float y) { return y < 0.f ? __fadd_rn(y, 1.f) : 1.f; }
 

@@ -264,6 +264,7 @@ struct ddpg_ctx {
     int tk_rpb = 0;          // DDPG_TK_RPB=n: thin_k row tiles per block (0: auto)
     bool kcomb = true;       // DDPG_KCOMB=0: no in-launch K split for small-M plain twin GEMMs
     int kc_blocks = 200;     // DDPG_KCOMB_BLOCKS=n: split plain twin GEMMs of fewer tiles
+    bool tk_fwd = true;      // DDPG_TK_FWD=0: thin_k's generic epilogue for forward parts too
     int kc_splits = 4;       // DDPG_KCOMB_SPLITS=s: at most s splits per tile (2 .. KC_MAXS)
   } sw;
 

@@ -505,10 +505,22 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
   }
   a.mt = mt;
   a.rpb = rpb;
+  // the forward twin-only form when every part is one (thin_k.h)
+  bool fwd = c->sw.tk_fwd && M % TK_ROWS == 0;
+  for (int i = 0; i < nparts; ++i) {
+    const TkPart& q = a.p[i];
+    fwd = fwd && q.bias && q.act == 1 && !q.out && q.outh && !q.aux && !q.colsum &&
+          q.N % TK_COLS == 0 && q.ldo % 8 == 0 && q.hps % 8 == 0 && ((uintptr_t)q.outh & 15) == 0;
+  }
   char key[96];
-  snprintf(key, sizeof key, "thin_k_kernel|%s", name);
+  snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : "", name);
   ProfScope ps(c, key, flops, bytes);
-  hipLaunchKernelGGL(thin_k_kernel, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0, c->cur, a);
+  if (fwd)
+    hipLaunchKernelGGL(thin_k_kernel<true>, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0,
+                       c->cur, a);
+  else
+    hipLaunchKernelGGL(thin_k_kernel<false>, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0,
+                       c->cur, a);
   HIP_TRY(hipGetLastError());
   return mt;
 }

@@ -22,6 +22,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       gemm_h3.h kernels combine in-launch K splits)
     DDPG_TK_RPB=3     thin_k blocks walk 3 row tiles each (W panel staged once,
                       next X tile prefetched) instead of the automatic count
+    DDPG_TK_FWD=0     thin_k's forward parts on the generic epilogue instead of the
+                      forward twin-only form (same arithmetic, flags folded away)
     DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
                       instead of read in place from the pinned host buffer
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
@@ -49,7 +51,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_M
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
-            "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN")
+            "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD")
 
 
 @pytest.fixture(scope="module")
@@ -135,6 +137,7 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_ACT32", "1", "wide"),
     ("DDPG_GEMM_H3", "0", "wide"),
     ("DDPG_TK_RPB", "3", "wide"),
+    ("DDPG_TK_FWD", "0", "wide"),
     ("DDPG_SLOTS_H2D", "1", "wide"),
     ("DDPG_SLOTS_H2D", "1", "ip"),
 ])
@@ -145,9 +148,12 @@ def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
         # kernels on the same unsplit plan
         monkeypatch.setenv("DDPG_KCOMB", "0")
     p, _ = _params(O, name)
-    ref = _run(dd, O, name, p, 3)
+    ref = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
     monkeypatch.setenv(switch, value)
-    got = _run(dd, O, name, p, 3)
+    got = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
+    if switch == "DDPG_TK_FWD":  # the default runs the forward form, the switch does not
+        assert any(k.startswith("thin_k_kernel<FWD>") for k in ref["keys"]), ref["keys"]
+        assert not any(k.startswith("thin_k_kernel<FWD>") for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 

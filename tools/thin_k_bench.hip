@@ -5,10 +5,17 @@
 #include <cstdio>
 #include <cstring>
 __device__ unsigned long long g_st[8192 * 5];
+// per-block phase clocks summed over the row walk: g_ph[b][i] += time since
+// the previous stamp of block b, for the stamp i that ends the phase
+__device__ unsigned long long g_ph[8192 * 8], g_last[8192];
 #define TK_STAMP(i)                                                                        \
-  if (threadIdx.x == 0)                                                                    \
-    g_st[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 5 + (i)] =      \
-        __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {                                                                  \
+    const int b_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);         \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
+    if ((i) < 4) g_st[b_ * 5 + (i)] = t_;                                                      \
+    if ((i) > 0) g_ph[b_ * 8 + (i)] += t_ - g_last[b_];                                    \
+    g_last[b_] = t_;                                                                       \
+  }
 #include "../distributed_ddpg_amd/csrc/thin_k.h"
 #ifdef WITH_OLD
 #include "../build_variants/thin_k_old.h"
@@ -17,6 +24,19 @@ __device__ unsigned long long g_st[8192 * 5];
 #include <algorithm>
 
 // per-phase block averages and whole-grid span of the LAST launch (core clocks)
+// per-phase clocks summed over each block's row walk, averaged over blocks:
+// [1] up to the tile barrier (first trip: W panel + X; later: colsum + next X
+// split), [2] MFMAs, [3] accumulators -> LDS + barrier, [4] the epilogue row
+// loop (LDS reads, element-wise, store issue)
+static void walk(const char* tag, int nblocks) {
+  std::vector<unsigned long long> h(nblocks * 8);
+  hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_ph), h.size() * 8);
+  double d[5] = {0, 0, 0, 0, 0};
+  for (int b = 0; b < nblocks; ++b)
+    for (int i = 1; i <= 4; ++i) d[i] += double(h[b * 8 + i]) / nblocks;
+  printf("   %s walk: to-barrier %.0f mfma %.0f acc->lds %.0f epilogue-loop %.0f clk/block\n", tag,
+         d[1], d[2], d[3], d[4]);
+}
 static void phases(const char* tag, int nblocks) {
   std::vector<unsigned long long> h(nblocks * 5);
   hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_st), h.size() * 8);
@@ -38,7 +58,7 @@ static void phases(const char* tag, int nblocks) {
 using namespace ddpg;
 
 typedef void (*tk_fn)(TkArgs);
-static tk_fn g_kern = thin_k_kernel;
+static tk_fn g_kern = thin_k_kernel<false>;
 static int g_rb = 0;  // row blocks of the kernel under test
 static float time_it(const TkArgs& a, int nparts, int reps) {
   hipEvent_t e0, e1;
@@ -53,6 +73,10 @@ static float time_it(const TkArgs& a, int nparts, int reps) {
   hipEventSynchronize(e1);
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
+  static std::vector<unsigned long long> z(8192 * 8, 0ull);
+  hipMemcpyToSymbol(HIP_SYMBOL(g_ph), z.data(), z.size() * 8);
+  hipLaunchKernelGGL(g_kern, grid, dim3(TK_NT), 0, 0, a);  // the launch phases() / walk() read
+  hipDeviceSynchronize();
   return 1e3f * ms / reps;
 }
 
@@ -69,7 +93,7 @@ int main() {
   run_all();
 #ifdef WITH_OLD
   printf("== old thin_k_kernel\n");
-  g_kern = old::thin_k_old_kernel;
+  g_kern = old::thin_k_old_kernel;  // (build_variants/, WITH_OLD only)
   g_rb = 4096 / 64;
   run_all();
 #endif
@@ -101,6 +125,7 @@ static void run_all() {
   a.p[0] = p;
   printf("K64 bias+elu+store           %.2f us\n", time_it(a, 1, 200));
   phases("K64", 8 * g_rb);
+  walk("K64", 8 * g_rb);
   {
     __bf16* tw;
     hipMalloc(&tw, (size_t)M * 2 * N * 2 * 3);
@@ -145,8 +170,17 @@ static void run_all() {
     }
     printf("5 parts twin-only K64x4|K16  %.2f us\n", time_it(a, 5, 100));
     phases("5 parts", 8 * g_rb * 5);
-    for (int i = 0; i < 5; ++i) a.p[i].outh = nullptr;
+    walk("5 parts", 8 * g_rb * 5);
+    g_kern = thin_k_kernel<true>;
+    printf("5 parts twin-only, FWD form  %.2f us\n", time_it(a, 5, 100));
+    walk("5 parts FWD", 8 * g_rb * 5);
+    g_kern = thin_k_kernel<false>;
+    for (int i = 0; i < 5; ++i) a.p[i].act = 0;
+    printf("5 parts twin-only, no elu    %.2f us\n", time_it(a, 5, 100));
+    walk("5 parts no elu", 8 * g_rb * 5);
+    for (int i = 0; i < 5; ++i) a.p[i].act = 1, a.p[i].outh = nullptr;
     printf("5 parts no store             %.2f us\n", time_it(a, 5, 100));
+    walk("5 parts no store", 8 * g_rb * 5);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
