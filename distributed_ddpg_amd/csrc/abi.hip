@@ -156,7 +156,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
       c->sw.gemm_h3 = !env_is("DDPG_GEMM_H3", "0");
-      if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = std::min(4, std::max(0, atoi(v)));
+      if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = atoi(v) == 1;
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");
@@ -166,6 +166,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       if (const char* v = getenv("DDPG_TK_RPB")) c->sw.tk_rpb = std::max(0, atoi(v));
       c->sw.kcomb = !env_is("DDPG_KCOMB", "0");
       c->sw.tk_fwd = !env_is("DDPG_TK_FWD", "0");
+      c->sw.gemm_pack = !env_is("DDPG_GEMM_PACK", "0");
+      c->sw.prof_shapes = env_is("DDPG_PROF_SHAPES", "1");
       if (const char* v = getenv("DDPG_KCOMB_BLOCKS"))
         c->sw.kc_blocks = std::min(kKcTickets, std::max(1, atoi(v)));
       if (const char* v = getenv("DDPG_KCOMB_SPLITS"))

@@ -147,6 +147,14 @@ struct ddpg_replay {
 void replay_flush(ddpg_replay* rb);
 
 // ====================================================================== context
+// a GEMM queued under gemm_defer (gemm_flush)
+struct DeferredGemm {
+  GemmHArgs a;
+  dim3 grid;
+  double flops, bytes;
+  char key[112];
+};
+
 struct ddpg_ctx {
   ddpg_cfg cfg{};
   Layout L;
@@ -254,7 +262,7 @@ struct ddpg_ctx {
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
     bool gemm_h3 = true;   // DDPG_GEMM_H3=0: twin GEMMs with runtime slot addressing (gemm_h_kernel / gemm_h16_kernel)
-    int gemm256 = 0;       // DDPG_GEMM256=1 / 4: bf16 split-K weight gradients on gemm_h256.h; 2, 3: more shapes
+    int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h (opt-in)
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs
@@ -264,6 +272,8 @@ struct ddpg_ctx {
     int tk_rpb = 0;          // DDPG_TK_RPB=n: thin_k row tiles per block (0: auto)
     bool kcomb = true;       // DDPG_KCOMB=0: no in-launch K split for small-M plain twin GEMMs
     int kc_blocks = 200;     // DDPG_KCOMB_BLOCKS=n: split plain twin GEMMs of fewer tiles
+    bool prof_shapes = false;  // DDPG_PROF_SHAPES=1: GEMM / thin_k profile keys carry shapes
+    bool gemm_pack = true;   // DDPG_GEMM_PACK=0: deferred GEMMs launched one by one
     bool tk_fwd = true;      // DDPG_TK_FWD=0: thin_k's generic epilogue for forward parts too
     int kc_splits = 4;       // DDPG_KCOMB_SPLITS=s: at most s splits per tile (2 .. KC_MAXS)
   } sw;
@@ -276,6 +286,8 @@ struct ddpg_ctx {
   size_t kc_part_n = 0;
   unsigned* kc_ticket = nullptr;
   int kc_rot = 0, kc_next = 0;
+  int gemm_defer = 0;  // > 0: gemm_launch queues gemm_h16i GEMMs for gemm_flush
+  std::vector<DeferredGemm> deferred;
   int tk_slots = 512;  // thin_k blocks resident at once (ddpg_create: CUs x blocks per CU)
 
   // comm: every collective of the ctx is issued on cs (one stream, so the
@@ -410,6 +422,7 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda, con
 TkPart tk_part(const float* X, int ldx, int K, const float* W, int ldw, int w_nk, int N,
                const float* bias, int act, float* out, int ldo);
 int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M);
+void gemm_flush(ddpg_ctx* c);
 GemmPlan wgrad_launch(ddpg_ctx* c, const float* A, int lda, const float* B, int ldb, int M, int N,
                       int K, float* slab, int cap, float* direct);
 // step.hip

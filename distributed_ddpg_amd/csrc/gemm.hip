@@ -185,20 +185,12 @@ static int h256_splits(int M, int N, int K, int cap) {
 // (DDPG_GEMM256=1); 1 / 2: unsplit GEMMs (=2 / =3).  Full tiles only.  Off by
 // default: in the C5 step the finer split's extra slab reduction cost more
 // than the faster main loop saved (profiles/r3/gemm_h256_ab_c5.txt).
-static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e,
-                     bool dx_layout, bool a_rk) {
+static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e) {
   if (!(c->hnp == 1 && c->sw.gemm256 && c->sw.gemm_mf == 16 && M % H2_BM == 0 &&
         N % H2_BN == 0 && Kh % 128 == 0))
     return -1;
   const bool plain = !e.bias && e.act == 0 && e.post == 0 && !e.colsum && !e.proj_out && !e.outh;
-  if (splits != 1) return plain ? 0 : -1;
-  // measurement switches (same-box A/B): DDPG_GEMM256=2 adds the
-  // >= 256-tile dX GEMMs (MODE 1); 3 also every unsplit GEMM of >= 128 tiles
-  // (MODE 2, relying on the step's concurrent streams to fill the chip)
-  const bool dx = !e.bias && e.act == 0 && e.post == 1;
-  const int tiles = (M / H2_BM) * (N / H2_BN);
-  if ((c->sw.gemm256 == 2 || c->sw.gemm256 == 3) && dx && dx_layout && tiles >= 256) return 1;
-  return c->sw.gemm256 == 3 && a_rk && tiles >= 128 ? 2 : -1;
+  return splits != 1 && plain ? 0 : -1;
 }
 
 // direct: for a split-K weight gradient, where to write the result when the
@@ -296,19 +288,14 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       a.xcd = xcd_rect(c, h.nt(N), h.mt(M), BMh, HG_BN);
       a.e = ee;
       static const char* lay[2] = {"RK", "KR"};
-      // bf16 configuration, whole 256 x 256 tiles (gemm_h256.h): the split-K
-      // weight gradients (plain slabs, MODE 0) and the dX GEMMs whose grid
-      // fills the chip unsplit (>= 256 tiles, MODE 1)
+      // bf16 configuration, opt-in DDPG_GEMM256=1: the split-K weight
+      // gradients on whole 256 x 256 tiles (gemm_h256.h, plain slabs, MODE 0)
       const int mode256 =
-          h256_mode(c, M, N, Kh, splits_req, ee_req, AL == L_RK && BL == L_RK, AL == L_RK);
+          h256_mode(c, M, N, Kh, splits_req, ee_req);
       if (mode256 >= 0) {
         GemmPlan q;
         q.bm = q.bn = H2_BM;
-        int sp = mode256 == 0 ? h256_splits(M, N, Kh, cap) : 1;
-        // DDPG_GEMM256=4: the 256 x 128 plan's split count (no extra slab to
-        // reduce; half the blocks, beside the concurrent dX chain)
-        if (mode256 == 0 && c->sw.gemm256 == 4 && Kh % h.splits == 0 && (Kh / h.splits) % 128 == 0)
-          sp = h.splits;
+        const int sp = h256_splits(M, N, Kh, cap);
         q.kps = Kh / sp;
         q.splits = sp;
         GemmEpi e2 = ee_req;
@@ -326,14 +313,7 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
         ProfScope ps(c, key, 2.0 * M * N * (double)K,
                      2.0 * ((double)M * K + (double)K * N) + 4.0 * (double)M * N * q.splits);
         const dim3 grid(q.nt(N), q.mt(M), q.splits);
-        if (mode256 == 0) {
-          hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 0>), grid, dim3(H2_NT), 0, c->cur, a);
-        } else if (mode256 == 2) {
-          if constexpr (AL == L_RK)
-            hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 2>), grid, dim3(H2_NT), 0, c->cur, a);
-        } else if constexpr (AL == L_RK && BL == L_RK) {
-          hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 1>), grid, dim3(H2_NT), 0, c->cur, a);
-        }
+        hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 0>), grid, dim3(H2_NT), 0, c->cur, a);
         HIP_TRY(hipGetLastError());
         return q;
       }
@@ -341,14 +321,30 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
       char key[112];
       // "/kc": the splits are combined in-launch (small-M plan)
-      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s%s",
+      // DDPG_PROF_SHAPES=1: the shape and split count in the key too
+      char shp[48] = "";
+      if (c->sw.prof_shapes) snprintf(shp, sizeof shp, " %dx%dx%d/%d", M, N, K, h.splits);
+      snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s%s%s",
                h16 ? (AL == L_RK && c->sw.gemm_h3 ? "gemm_h16i_kernel" : "gemm_h16_kernel")
                    : (c->hnp == 3 && c->sw.gemm_h3) ? "gemm_h3_kernel" : "gemm_h_kernel",
-               lay[AL], lay[BL], c->hnp, name, a.kpart ? "/kc" : "");
-      ProfScope ps(c, key, 2.0 * M * N * (double)K,
-                   2.0 * c->hnp * ((double)M * K + (double)K * N) +
-                       4.0 * (double)M * N * h.splits);
+               lay[AL], lay[BL], c->hnp, name, a.kpart ? "/kc" : "", shp);
       const dim3 grid(h.nt(N), h.mt(M), h.splits);
+      const double fl = 2.0 * M * N * (double)K,
+                   by = 2.0 * c->hnp * ((double)M * K + (double)K * N) + 4.0 * (double)M * N * h.splits;
+      if constexpr (AL == L_RK && BL == L_KR) {
+        // gemm_defer (first_layers_dev): queue for one gemm_h16i_pack_kernel launch
+        if (c->gemm_defer && h16 && c->sw.gemm_h3 && h.splits == 1 && !a.kpart) {
+          DeferredGemm d;
+          d.a = a;
+          d.grid = grid;
+          d.flops = fl;
+          d.bytes = by;
+          snprintf(d.key, sizeof d.key, "%s", key);
+          c->deferred.push_back(d);
+          return h;
+        }
+      }
+      ProfScope ps(c, key, fl, by);
       if (h16 && AL == L_RK && c->sw.gemm_h3) {
         // immediate-offset addressing (gemm_h3.h), RK A operands
         if constexpr (AL == L_RK)
@@ -459,6 +455,40 @@ TkPart tk_part(const float* X, int ldx, int K, const float* W, int ldw, int w_nk
 // Launch 1 .. TK_MAXP thin-K parts over M rows; returns the number of 64-row
 // blocks (the row count of colsum partials), or 0 (nothing launched) when a
 // layer is not eligible and the caller must use the GEMM.
+// Launch the GEMMs queued under gemm_defer: one gemm_h16i_pack_kernel launch
+// per GH_MAXP of them when they share a grid (DDPG_GEMM_PACK=0: one launch
+// each, the same kernel body), in queue order.
+void gemm_flush(ddpg_ctx* c) {
+  std::vector<DeferredGemm> q;
+  q.swap(c->deferred);
+  size_t i = 0;
+  while (i < q.size()) {
+    size_t n = 1;
+    while (c->sw.gemm_pack && i + n < q.size() && n < (size_t)GH_MAXP &&
+           q[i + n].grid.x == q[i].grid.x && q[i + n].grid.y == q[i].grid.y)
+      ++n;
+    if (n == 1) {
+      ProfScope ps(c, q[i].key, q[i].flops, q[i].bytes);
+      hipLaunchKernelGGL((gemm_h16i_kernel<L_RK, L_KR>), q[i].grid, dim3(HG_NT), 0, c->cur, q[i].a);
+    } else {
+      GemmHPack pk;
+      double fl = 0, by = 0;
+      for (size_t j = 0; j < n; ++j) {
+        pk.p[j] = q[i + j].a;
+        fl += q[i + j].flops;
+        by += q[i + j].bytes;
+      }
+      char key[128];
+      snprintf(key, sizeof key, "gemm_h16i_pack_kernel<RK,KR,NP=1>|%s", strchr(q[i].key, '|') + 1);
+      ProfScope ps(c, key, fl, by);
+      hipLaunchKernelGGL((gemm_h16i_pack_kernel<L_RK, L_KR>), dim3(q[i].grid.x, q[i].grid.y, n),
+                         dim3(HG_NT), 0, c->cur, pk);
+    }
+    HIP_TRY(hipGetLastError());
+    i += n;
+  }
+}
+
 int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M) {
   if (!c->sw.thin_k || nparts < 1 || nparts > TK_MAXP) return 0;
   TkPart pp[TK_MAXP];
@@ -505,15 +535,18 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
   }
   a.mt = mt;
   a.rpb = rpb;
-  // the forward twin-only form when every part is one (thin_k.h)
+  // the forward form when every part is one (thin_k.h)
   bool fwd = c->sw.tk_fwd && M % TK_ROWS == 0;
   for (int i = 0; i < nparts; ++i) {
     const TkPart& q = a.p[i];
-    fwd = fwd && q.bias && q.act == 1 && !q.out && q.outh && !q.aux && !q.colsum &&
+    fwd = fwd && q.bias && q.act == 1 && q.outh && !q.aux && !q.colsum &&
           q.N % TK_COLS == 0 && q.ldo % 8 == 0 && q.hps % 8 == 0 && ((uintptr_t)q.outh & 15) == 0;
   }
   char key[96];
   snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : "", name);
+  if (c->sw.prof_shapes)
+    snprintf(key + strlen(key), sizeof key - strlen(key), " %dp %dx%dx%d", nparts, M, parts[0].N,
+             parts[0].K);
   ProfScope ps(c, key, flops, bytes);
   if (fwd)
     hipLaunchKernelGGL(thin_k_kernel<true>, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0,

@@ -39,23 +39,8 @@ DDPG_DEV void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-struct GemmHArgs {
-  const __bf16* A;
-  const __bf16* B;
-  long long pa, pb;  // elements between planes (NP = 3)
-  int M, N, K, lda, ldb;
-  int kps;  // k extent per split (multiple of BK)
-  int xcd;
-  GemmEpi e;
-  // in-launch K split (ksplit_combine, gemm_h3_kernel / gemm_h16i_kernel):
-  // partials [tile][split] and one ticket per output tile; null: the splits
-  // are separate slabs (weight gradients) or there is one split
-  float* kpart = nullptr;
-  unsigned* kticket = nullptr;
-#ifdef DDPG_KC_STAMPS
-  unsigned long long* stamps = nullptr;  // tools/kc_bench.hip only: per-block phase clocks
-#endif
-};
+// GemmHArgs: types.h
+
 
 constexpr int HG_NT = 512, HG_BN = 128, HG_STAGES = 3;
 

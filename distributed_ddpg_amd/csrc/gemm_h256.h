@@ -29,9 +29,11 @@
 // loop is unrolled by the 4 slots so every LDS address is an immediate
 // offset and the two fragment register sets alternate statically.
 //
-// Used where the grid fills the chip without a K split: plain GEMMs with at
-// least 256 output tiles (C5's N = 4096 dX), and the split-K weight gradients
-// (MODE 0, each split's fp32 slab reduced by the Adam-side slab reduction).
+// The product instantiates MODE 0 only, behind the opt-in DDPG_GEMM256=1: the
+// split-K weight gradients (each split's fp32 slab reduced by the Adam-side
+// slab reduction).  MODE 1 / 2 (fused epilogues, one split) are built by
+// tools/gemmh256_bench.hip alone: 1.19x gemm_h16 on the N = 4096 dX in
+// isolation, no faster inside the C5 step.
 // The 128-tile C5 shapes (4096 x 2048 outputs) stay on gemm_h16_kernel: an
 // in-launch combine of two K-halves (ticketed first / last arriver, the first
 // arriver's fp32 partial through write-through stores) measured 0.75-0.92x

@@ -310,7 +310,7 @@ namespace ddpg {
 // schedule and MFMA order: bitwise equal to gemm_h16_kernel
 // (DDPG_GEMM_H3=0 selects it).
 template <int AL, int BL>
-__global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_kernel(GemmHArgs g) {
+DDPG_DEV void gemm_h16i_body(const GemmHArgs& g, int z) {
   static_assert(AL == L_RK, "RK A operand");
   constexpr int NP = 1, BM = 256, BK = 64;
   using C = HgCfg<BM, BK, NP>;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_kernel(GemmHArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
   int bx, by;
   xcd_tile(bx, by, g.xcd);
-  const int n0 = bx * HG_BN, m0 = by * BM, z = blockIdx.z;
+  const int n0 = bx * HG_BN, m0 = by * BM;
   const int kbeg = z * g.kps;
   const int kend = min(g.K, kbeg + g.kps);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
@@ -516,6 +516,22 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_kernel(GemmHArgs g) {
   ge.N = g.N;
   ge.e = g.e;
   gemm_epilogue<BM, HG_BN, 4, 16>(out, smem, ge, tid, n0, m0, ze, bx, by);
+}
+
+template <int AL, int BL>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_kernel(GemmHArgs g) {
+  gemm_h16i_body<AL, BL>(g, blockIdx.z);
+}
+
+// Up to GH_MAXP independent GEMMs of one grid shape in one launch, part =
+// blockIdx.z (one split each, no in-launch combine): the batch-only first
+// layers of the bf16 configuration (K = S > 64, so not thin_k's).  A CU's
+// next block (the next part's tile) stages and computes while the previous
+// block's epilogue stores drain, where separate launches wrote every output
+// in one burst at the end of each.
+template <int AL, int BL>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h16i_pack_kernel(GemmHPack pk) {
+  gemm_h16i_body<AL, BL>(pk.p[blockIdx.z], 0);
 }
 
 }  // namespace ddpg

@@ -613,7 +613,27 @@ static bool first_layers_dev(ddpg_ctx* c, int B) {
   critic_l1_parts(c, c->theta, c->s, c->a, B, c->cat, tc);
   tp[3] = tc[0];
   tp[4] = tc[1];
-  return thin_k_launch(c, "fwd_l1", tp, TK_MAXP, B) != 0;
+  if (thin_k_launch(c, "fwd_l1", tp, TK_MAXP, B)) return true;
+  // S > 64 (the bf16 configuration C5: S = 376): each part on thin_k where
+  // it takes it, the rest as ONE gemm_h16i_pack_kernel launch (gemm_flush)
+  if (!(c->hnp == 1 && c->sw.gemm_h3 && c->sw.gemm_mf == 16)) return false;
+  c->gemm_defer = 1;
+  for (int i = 0; i < TK_MAXP; ++i) {
+    if (thin_k_launch(c, "fwd_l1", &tp[i], 1, B)) continue;
+    GemmEpi e = epi_none();
+    e.out = tp[i].out;
+    e.outh = tp[i].outh;
+    e.h_plane_stride = tp[i].hps;
+    e.h_planes = c->hnp;
+    e.ldo = tp[i].ldo;
+    e.bias = tp[i].bias;
+    e.act = tp[i].act;
+    gemm_launch<L_RK, L_KR>(c, "fwd_l1", tp[i].X, tp[i].ldx, tp[i].W, tp[i].ldw, B, tp[i].N,
+                            tp[i].K, e);
+  }
+  c->gemm_defer = 0;
+  gemm_flush(c);
+  return true;
 }
 
 static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {

@@ -53,8 +53,8 @@ DDPG_DEV int tk_oidx(int r, int n) {
 // (its global loads in flight under the current tile's MFMAs and epilogue
 // stores), so the stream of output stores -- what bounds these layers -- is
 // not interrupted by a fresh W-panel round trip per 64 rows.
-// FWD = true: the forward twin-only form (every part: bias, elu, the twin
-// as whole 8-column octets, no fp32 copy, no aux, no column sums, full row
+// FWD = true: the forward form (every part: bias, elu, the twin as whole
+// 8-column octets, an fp32 copy or none, no aux, no column sums, full row
 // and column tiles -- thin_k_launch checks), with the epilogue's runtime
 // flags and bounds folded away: that row loop is VALU-bound.
 template <bool FWD>
@@ -256,6 +256,10 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
       const float4 va = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]);
       const float4 vb = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
       if (FWD) {
+        if (P.out) {
+          *reinterpret_cast<f32x4*>(P.out + o) = v[0];
+          *reinterpret_cast<f32x4*>(P.out + o + 4) = v[1];
+        }
         store_twin8(P.outh + o, P.hps, P.hnp, va, vb);
         continue;
       }

@@ -153,4 +153,29 @@ struct SbGradTab {
   float* sh;
 };
 
+// twin-GEMM launch arguments (gemm_h.h, gemm_h3.h)
+struct GemmHArgs {
+  const __bf16* A;
+  const __bf16* B;
+  long long pa, pb;  // elements between planes (NP = 3)
+  int M, N, K, lda, ldb;
+  int kps;  // k extent per split (multiple of BK)
+  int xcd;
+  GemmEpi e;
+  // in-launch K split (ksplit_combine, gemm_h3_kernel / gemm_h16i_kernel):
+  // partials [tile][split] and one ticket per output tile; null: the splits
+  // are separate slabs (weight gradients) or there is one split
+  float* kpart = nullptr;
+  unsigned* kticket = nullptr;
+#ifdef DDPG_KC_STAMPS
+  unsigned long long* stamps = nullptr;  // tools/kc_bench.hip only: per-block phase clocks
+#endif
+};
+
+// independent GEMMs of one grid shape launched together (gemm_h16i_pack_kernel)
+constexpr int GH_MAXP = 4;
+struct GemmHPack {
+  GemmHArgs p[GH_MAXP];
+};
+
 }  // namespace ddpg

@@ -59,6 +59,8 @@ CONFIGS = {
     "mc": (2, 1, 48, 64, 1.0, 64, "mc_model120"),
     "odd": (5, 3, 40, 72, 2.0, 37, None),
     "wide": (64, 16, 1024, 1024, 1.0, 256, None),
+    # S > 64: the first layers on the GEMMs, not thin_k
+    "wides": (200, 16, 1024, 1024, 1.0, 256, None),
 }
 # the MountainCar checkpoint's critic is 48/128 while its actor is 48/64
 CRITIC_W = {"mc": (48, 128)}

@@ -22,6 +22,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       gemm_h3.h kernels combine in-launch K splits)
     DDPG_TK_RPB=3     thin_k blocks walk 3 row tiles each (W panel staged once,
                       next X tile prefetched) instead of the automatic count
+    DDPG_GEMM_PACK=0  the bf16 configuration's S > 64 first layers launched one
+                      by one instead of as one gemm_h16i_pack_kernel launch
     DDPG_TK_FWD=0     thin_k's forward parts on the generic epilogue instead of the
                       forward twin-only form (same arithmetic, flags folded away)
     DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
@@ -51,7 +53,8 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_M
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
-            "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD")
+            "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
+            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK")
 
 
 @pytest.fixture(scope="module")
@@ -170,6 +173,37 @@ def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
     got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
     assert any(k.startswith("gemm_h_kernel") and "NP=1" in k for k in got["keys"]), got["keys"]
     assert not any(k.startswith("gemm_h16_kernel") for k in got["keys"]), got["keys"]
+    _bitwise(got, ref)
+
+
+def test_tk_fwd_bf16_bitwise(dd, O, monkeypatch):
+    """bf16 configuration (fp32 activation copies beside the bf16 twins): the
+    thin_k forward form with its fp32 copy against the generic epilogue
+    (DDPG_TK_FWD=0) -- bitwise after 2 fused steps."""
+    _clear(monkeypatch)
+    p, _ = _params(O, "wide")
+    ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
+    assert any(k.startswith("thin_k_kernel<FWD>") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_TK_FWD", "0")
+    got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
+    assert not any(k.startswith("thin_k_kernel<FWD>") for k in got["keys"]), got["keys"]
+    _bitwise(got, ref)
+
+
+def test_gemm_pack_bf16_bitwise(dd, O, monkeypatch):
+    """bf16 configuration with S = 200 (first layers on the GEMMs): the four
+    batch-only K = S first layers as one gemm_h16i_pack_kernel launch by
+    default, one gemm_h16i_kernel launch each with DDPG_GEMM_PACK=0 -- the same
+    kernel body per tile, bitwise equal after 2 fused steps.  DDPG_KCOMB=0
+    keeps B = 256 on the unsplit plan the pack takes."""
+    _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_KCOMB", "0")
+    p, _ = _params(O, "wides")
+    ref = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
+    assert any(k.startswith("gemm_h16i_pack_kernel") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_GEMM_PACK", "0")
+    got = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
+    assert not any(k.startswith("gemm_h16i_pack_kernel") for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 

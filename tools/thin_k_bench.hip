@@ -91,6 +91,9 @@ int main() {
   printf("== thin_k_kernel, 6 row tiles per block\n");
   g_rb = (4096 / TK_ROWS + 5) / 6;
   run_all();
+  printf("== thin_k_kernel, 8 row tiles per block\n");
+  g_rb = 4096 / TK_ROWS / 8;
+  run_all();
 #ifdef WITH_OLD
   printf("== old thin_k_kernel\n");
   g_kern = old::thin_k_old_kernel;  // (build_variants/, WITH_OLD only)
