@@ -535,25 +535,28 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
   }
   a.mt = mt;
   a.rpb = rpb;
-  // the forward form when every part is one (thin_k.h)
-  bool fwd = c->sw.tk_fwd && M % TK_ROWS == 0;
+  // the forward / backward forms when every part is one (thin_k.h)
+  bool fwd = c->sw.tk_fwd && M % TK_ROWS == 0, bwd = fwd;
   for (int i = 0; i < nparts; ++i) {
     const TkPart& q = a.p[i];
-    fwd = fwd && q.bias && q.act == 1 && q.outh && !q.aux && !q.colsum &&
-          q.N % TK_COLS == 0 && q.ldo % 8 == 0 && q.hps % 8 == 0 && ((uintptr_t)q.outh & 15) == 0;
+    const bool full = q.N % TK_COLS == 0 && q.ldo % 8 == 0 &&
+                      (!q.outh || (q.hps % 8 == 0 && ((uintptr_t)q.outh & 15) == 0));
+    fwd = fwd && full && q.bias && q.act == 1 && q.outh && !q.aux && !q.colsum;
+    bwd = bwd && full && !q.bias && q.act == 0 && q.aux && q.colsum && q.ldaux % 4 == 0;
   }
   char key[96];
-  snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : "", name);
+  snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : bwd ? "<BWD>" : "", name);
   if (c->sw.prof_shapes)
     snprintf(key + strlen(key), sizeof key - strlen(key), " %dp %dx%dx%d", nparts, M, parts[0].N,
              parts[0].K);
   ProfScope ps(c, key, flops, bytes);
+  const dim3 grid(nc, ceil_div(mt, rpb), nparts);
   if (fwd)
-    hipLaunchKernelGGL(thin_k_kernel<true>, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0,
-                       c->cur, a);
+    hipLaunchKernelGGL(thin_k_kernel<1>, grid, dim3(TK_NT), 0, c->cur, a);
+  else if (bwd)
+    hipLaunchKernelGGL(thin_k_kernel<2>, grid, dim3(TK_NT), 0, c->cur, a);
   else
-    hipLaunchKernelGGL(thin_k_kernel<false>, dim3(nc, ceil_div(mt, rpb), nparts), dim3(TK_NT), 0,
-                       c->cur, a);
+    hipLaunchKernelGGL(thin_k_kernel<0>, grid, dim3(TK_NT), 0, c->cur, a);
   HIP_TRY(hipGetLastError());
   return mt;
 }

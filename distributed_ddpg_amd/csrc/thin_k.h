@@ -53,11 +53,13 @@ DDPG_DEV int tk_oidx(int r, int n) {
 // (its global loads in flight under the current tile's MFMAs and epilogue
 // stores), so the stream of output stores -- what bounds these layers -- is
 // not interrupted by a fresh W-panel round trip per 64 rows.
-// FWD = true: the forward form (every part: bias, elu, the twin as whole
-// 8-column octets, an fp32 copy or none, no aux, no column sums, full row
-// and column tiles -- thin_k_launch checks), with the epilogue's runtime
-// flags and bounds folded away: that row loop is VALU-bound.
-template <bool FWD>
+// MODE 0: every part's flags read at run time.  MODE 1, the forward form:
+// every part has bias, elu, the twin as whole 8-column octets, an fp32 copy
+// or none, no aux, no column sums, full row and column tiles.  MODE 2, the
+// backward form (dz2 = dz3 . W3^T): no bias, no activation, the EluGrad aux,
+// column sums, full tiles.  thin_k_launch checks; the folded flags and bounds
+// matter because the epilogue row loop is VALU-bound.
+template <int MODE>
 __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   __shared__ __attribute__((aligned(16))) char lds[TK_LDS];
   char* const wimg = lds;
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
     constexpr int RPT = TK_ROWS / TK_RG;  // rows per thread
     f32x4 aq[RPT][2];
-    if (!FWD && P.aux) {  // all aux loads in flight before the first use
+    if (MODE == 2 || (MODE == 0 && P.aux)) {  // all aux loads in flight before the first use
 #pragma unroll
       for (int i = 0; i < RPT; ++i) {
         const int m = m0 + rg + TK_RG * i;
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int rl = rg + TK_RG * i, m = m0 + rl;
-      if (!FWD && (!q0 || m >= M)) continue;
+      if (MODE == 0 && (!q0 || m >= M)) continue;
       f32x4 v[2];
       v[0] = *reinterpret_cast<const f32x4*>(Os + tk_oidx(rl, 8 * c8));
       v[1] = *reinterpret_cast<const f32x4*>(Os + tk_oidx(rl, 8 * c8 + 4));
@@ -246,21 +248,21 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float x = v[u][e];
-          if (FWD || P.bias) x = __fadd_rn(x, u ? bq1[e] : bq0[e]);
-          if (FWD || P.act == 1) x = elu_f(x);
-          if (!FWD && P.aux) x = __fmul_rn(x, elu_grad_factor(aq[i][u][e]));
+          if (MODE == 1 || (MODE == 0 && P.bias)) x = __fadd_rn(x, u ? bq1[e] : bq0[e]);
+          if (MODE == 1 || (MODE == 0 && P.act == 1)) x = elu_f(x);
+          if (MODE == 2 || (MODE == 0 && P.aux)) x = __fmul_rn(x, elu_grad_factor(aq[i][u][e]));
           v[u][e] = x;
-          if (!FWD && (u == 0 || q1)) csum[4 * u + e] += x;
+          if (MODE == 2 || (MODE == 0 && (u == 0 || q1))) csum[4 * u + e] += x;
         }
       const size_t o = (size_t)m * P.ldo + n;
       const float4 va = make_float4(v[0][0], v[0][1], v[0][2], v[0][3]);
       const float4 vb = make_float4(v[1][0], v[1][1], v[1][2], v[1][3]);
-      if (FWD) {
+      if (MODE != 0) {
         if (P.out) {
           *reinterpret_cast<f32x4*>(P.out + o) = v[0];
           *reinterpret_cast<f32x4*>(P.out + o + 4) = v[1];
         }
-        store_twin8(P.outh + o, P.hps, P.hnp, va, vb);
+        if (MODE == 1 || P.outh) store_twin8(P.outh + o, P.hps, P.hnp, va, vb);
         continue;
       }
       if (P.out) {
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
     }
     TK_STAMP(4);
     __syncthreads();  // output tile read: the region is next the column-sum scratch / X image
-    if (!FWD && P.colsum) {
+    if (MODE == 2 || (MODE == 0 && P.colsum)) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[rg * TK_COLS + 8 * c8 + e] = csum[e];
       __syncthreads();

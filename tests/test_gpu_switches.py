@@ -24,8 +24,9 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       next X tile prefetched) instead of the automatic count
     DDPG_GEMM_PACK=0  the bf16 configuration's S > 64 first layers launched one
                       by one instead of as one gemm_h16i_pack_kernel launch
-    DDPG_TK_FWD=0     thin_k's forward parts on the generic epilogue instead of the
-                      forward twin-only form (same arithmetic, flags folded away)
+    DDPG_TK_FWD=0     thin_k's forward and backward parts on the generic epilogue
+                      instead of the forward / backward forms (same arithmetic,
+                      flags and bounds folded away)
     DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
                       instead of read in place from the pinned host buffer
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
@@ -154,9 +155,11 @@ def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     ref = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
     monkeypatch.setenv(switch, value)
     got = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
-    if switch == "DDPG_TK_FWD":  # the default runs the forward form, the switch does not
-        assert any(k.startswith("thin_k_kernel<FWD>") for k in ref["keys"]), ref["keys"]
-        assert not any(k.startswith("thin_k_kernel<FWD>") for k in got["keys"]), got["keys"]
+    if switch == "DDPG_TK_FWD":  # the default runs both forms, the switch neither
+        for form in ("<FWD>", "<BWD>"):
+            assert any(k.startswith("thin_k_kernel" + form) for k in ref["keys"]), ref["keys"]
+        assert not any(k.startswith(("thin_k_kernel<FWD>", "thin_k_kernel<BWD>"))
+                       for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 

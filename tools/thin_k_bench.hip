@@ -58,7 +58,7 @@ static void phases(const char* tag, int nblocks) {
 using namespace ddpg;
 
 typedef void (*tk_fn)(TkArgs);
-static tk_fn g_kern = thin_k_kernel<false>;
+static tk_fn g_kern = thin_k_kernel<0>;
 static int g_rb = 0;  // row blocks of the kernel under test
 static float time_it(const TkArgs& a, int nparts, int reps) {
   hipEvent_t e0, e1;
@@ -174,10 +174,10 @@ static void run_all() {
     printf("5 parts twin-only K64x4|K16  %.2f us\n", time_it(a, 5, 100));
     phases("5 parts", 8 * g_rb * 5);
     walk("5 parts", 8 * g_rb * 5);
-    g_kern = thin_k_kernel<true>;
+    g_kern = thin_k_kernel<1>;
     printf("5 parts twin-only, FWD form  %.2f us\n", time_it(a, 5, 100));
     walk("5 parts FWD", 8 * g_rb * 5);
-    g_kern = thin_k_kernel<false>;
+    g_kern = thin_k_kernel<0>;
     for (int i = 0; i < 5; ++i) a.p[i].act = 0;
     printf("5 parts twin-only, no elu    %.2f us\n", time_it(a, 5, 100));
     walk("5 parts no elu", 8 * g_rb * 5);
