@@ -174,7 +174,8 @@ DDPG_DEV void store_twin(const GemmEpi& e, size_t i, float4 v) {
 // (bias-gradient column sums, thin projections).
 // PR: tile rows staged through LDS per pass (default BM / 2, one wave row;
 // BM / 4 for the 256 x 256 tile of gemm_h256.h, whose full wave row would not
-// fit beside the projection weights): smem must hold
+// fit beside the projection weights; BM for gemm_h3_kernel's 128-row tile:
+// one pass, every thread busy in the projection): smem must hold
 // PR * (BN + 4) + BN * PROJ_MAX + 2 * GNT floats.
 // ONLY >= 0: compile just that element-wise variant (the order of the
 // dispatch below; the caller guarantees the flags), fewer live registers.
@@ -187,8 +188,8 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   constexpr int NT = 2 * WGN * 64;  // threads
   constexpr int TM = BM / 64, TN = BN / (32 * WGN);
   constexpr int WR = BM / 2, WC = BN / WGN;
-  constexpr int PPW = WR / PR;  // passes per wave row
-  static_assert(PR <= WR && WR % PR == 0 && PR % 32 == 0, "pass rows");
+  constexpr int NPASS = BM / PR;
+  static_assert(BM % PR == 0 && PR % 32 == 0, "pass rows");
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave / WGN, wn = wave % WGN;
   const GemmEpi& e = g.e;
@@ -242,18 +243,17 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   // one LDS pass of PR rows (unrolled: a runtime pass index sends the
   // accumulators to scratch)
   auto do_pass = [&](int pass) {
-    if (wm == pass / PPW) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        if ((i * 32) / PR != pass % PPW) continue;  // this pass's 32-row blocks
+    for (int i = 0; i < TM; ++i) {
+      const int r0 = wm * WR + i * 32;  // this 32-row block's first tile row
+      if (r0 / PR != pass) continue;     // (wave-uniform) not in this pass
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = i * 32 - (pass % PPW) * PR + acc_row<MF>(r, lane);
-            Vs[rl * VS_LD + wn * WC + j * 32 + acc_col<MF>(r, lane)] = acc[i][j][r];
-          }
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int rl = r0 - pass * PR + acc_row<MF>(r, lane);
+          Vs[rl * VS_LD + wn * WC + j * 32 + acc_col<MF>(r, lane)] = acc[i][j][r];
+        }
     }
     __syncthreads();
     if ((outp || e.outh) && oct) {
@@ -336,7 +336,7 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
     __syncthreads();
   };
 #pragma unroll
-  for (int pass = 0; pass < 2 * PPW; ++pass) do_pass(pass);
+  for (int pass = 0; pass < NPASS; ++pass) do_pass(pass);
   if (e.colsum) {
     red[tid] = csum;
     __syncthreads();

@@ -12,7 +12,7 @@ timeout -k 10 200 python -u tools/gpu/keys.py c5 20 > gpurun_out/keys_c5_pack.tx
 head -14 gpurun_out/keys_c5_pack.txt; tail -1 gpurun_out/keys_c5_pack.txt
 timeout -k 10 200 python -u tools/gpu/keys.py c3 20 > gpurun_out/keys_c3_r4.txt 2> gpurun_out/keys_c3_r4.err || { tail gpurun_out/keys_c3_r4.err; exit 1; }
 grep thin_k gpurun_out/keys_c3_r4.txt; tail -1 gpurun_out/keys_c3_r4.txt
-timeout -k 10 400 python -u bench.py > gpurun_out/bench_r4.json 2> gpurun_out/bench_r4.err || { tail gpurun_out/bench_r4.err; exit 1; }
+T0=$(date +%s); timeout -k 10 400 python -u bench.py > gpurun_out/bench_r4.json 2> gpurun_out/bench_r4.err || { tail gpurun_out/bench_r4.err; exit 1; }; echo "bench wall $(( $(date +%s) - T0 )) s"
 python3 - <<'PY'
 import json
 d = json.load(open("gpurun_out/bench_r4.json"))
@@ -23,3 +23,4 @@ sb = d.get("small_batch", {})
 print("C2", sb.get("value"), sb.get("step_latency"))
 print("strong8", d["projected_scaling"]["strong"]["8"]["speedup_vs_1gpu"], "weak8", d["projected_scaling"]["weak"]["8"]["speedup_vs_1gpu"])
 PY
+echo "== one-pass epilogue A/B (A = two passes, B = one)"; bash tools/gpu/ab.sh c3 3 2>&1 | tee gpurun_out/epi1pass_ab_c3.txt
