@@ -83,14 +83,29 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
 
 // ---------------------------------------------------------------- thin heads
 // actor output: o = tanh(sum_t part[t][b][a]); mu = o * scale  (networks.py:59-61)
+// Sum of NT strided slab values in slab order (z = ((v0 + v1) + v2) + ...),
+// with the loads of up to 8 slabs in flight at once: a plain loop over a
+// runtime count made hipcc wait for each load before issuing the next, one
+// memory round trip per slab.
+DDPG_DEV float slab_sum(const float* __restrict__ p, int NT, size_t stride, float z) {
+  for (int t0 = 0; t0 < NT; t0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = t0 + i < NT ? p[(size_t)(t0 + i) * stride] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (t0 + i < NT) z += v[i];
+  }
+  return z;
+}
+
 __global__ void actor_out_kernel(const float* __restrict__ part, int NT, int B, int A,
                                  float scale, float* __restrict__ o, float* __restrict__ mu,
                                  int ld) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * A) return;
   const int b = i / A, a = i - b * A;
-  float z = 0.f;
-  for (int tt = 0; tt < NT; ++tt) z += part[((size_t)tt * B + b) * A + a];
+  const float z = slab_sum(part + (size_t)b * A + a, NT, (size_t)B * A, 0.f);
   const float ov = tanhf(z);
   if (o) o[(size_t)b * ld + a] = ov;
   if (mu) mu[(size_t)b * ld + a] = __fmul_rn(ov, scale);
@@ -105,8 +120,7 @@ __global__ void critic_q_kernel(const float* __restrict__ qpart, int NT, int B,
                                 float* __restrict__ y) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  float z = 0.f;
-  for (int tt = 0; tt < NT; ++tt) z += qpart[(size_t)tt * B + b];
+  float z = slab_sum(qpart + b, NT, (size_t)B, 0.f);
   z = __fadd_rn(z, bo[0]);
   if (q) q[b] = z;
   if (mode == 1) y[b] = (t[b] != 0.f) ? r[b] : __fadd_rn(r[b], __fmul_rn(gamma, z));
@@ -140,8 +154,7 @@ __global__ __launch_bounds__(256) void critic_loss_kernel(
   if (b < B) {
     float yb;
     if (td.qpart) {
-      float zt = 0.f;
-      for (int tt = 0; tt < td.NT; ++tt) zt += td.qpart[(size_t)tt * B + b];
+      float zt = slab_sum(td.qpart + b, td.NT, (size_t)B, 0.f);
       zt = __fadd_rn(zt, td.bo[0]);
       yb = (td.t[b] != 0.f) ? td.r[b] : __fadd_rn(td.r[b], __fmul_rn(td.gamma, zt));
       y[b] = yb;
@@ -323,8 +336,7 @@ __global__ void action_grad_kernel(const float* __restrict__ part, int NT, int B
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * A) return;
   const int b = i / A, a = i - b * A;
-  float g = 0.f;
-  for (int tt = 0; tt < NT; ++tt) g += part[((size_t)tt * ld_part_b + b) * A + a];
+  const float g = slab_sum(part + (size_t)b * A + a, NT, (size_t)ld_part_b * A, 0.f);
   if (da) da[(size_t)b * ld + a] = g;
   if (dz3) {
     const float ov = o[(size_t)b * ld + a];

@@ -23,4 +23,4 @@ sb = d.get("small_batch", {})
 print("C2", sb.get("value"), sb.get("step_latency"))
 print("strong8", d["projected_scaling"]["strong"]["8"]["speedup_vs_1gpu"], "weak8", d["projected_scaling"]["weak"]["8"]["speedup_vs_1gpu"])
 PY
-echo "== one-pass epilogue A/B (A = two passes, B = one)"; bash tools/gpu/ab.sh c3 3 2>&1 | tee gpurun_out/epi1pass_ab_c3.txt
+echo "== A/B: A = round-4 commit a3be9e4, B = + one-pass epilogue + slab_sum loads ahead"; bash tools/gpu/ab.sh c3 3 2>&1 | tee gpurun_out/epi1pass_ab_c3.txt
