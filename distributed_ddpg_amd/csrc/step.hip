@@ -155,6 +155,20 @@ static Twin critic_l1_parts(ddpg_ctx* c, const float* base, const float* s, cons
       tp[i].hps = ct.ps;
       tp[i].hnp = c->hnp;
     }
+  // cat2 (the critic at (s, mu), networks.py:143) with one bf16 plane: its
+  // fp32 values are read only as the action half's EluGrad operand (the
+  // action-gradient dX), so the state half writes its twin alone when the
+  // hidden layer reads the twin
+  if (!ct.p && cat == c->cat2 && c->hnp == 1 && c->sw.twin_only_cat2) {
+    const Twin t2 = act_twin(c, cat);
+    if (t2.p && gemm_h_ok<L_RK, L_KR>(c, cat, c->ldC, P(c, base, L.c[CWH]), c->CH2, B, c->CH2,
+                                      2 * c->CH1, 1, &kh)) {
+      tp[0].out = nullptr;
+      tp[0].outh = t2.p;
+      tp[0].hps = t2.ps;
+      tp[0].hnp = c->hnp;
+    }
+  }
   return ct;
 }
 
@@ -185,8 +199,9 @@ static int critic_fwd(ddpg_ctx* c, const float* base, const float* s, const floa
     e.h_plane_stride = ct.ps;
     e.h_planes = c->hnp;
     if (!thin_k_launch(c, "fwd", &tp[0], 1, B)) {
-      e.out = ct.p ? nullptr : cat;
-      e.outh = ct.p;
+      e.out = tp[0].out;  // as critic_l1_parts chose (fp32 and / or twin)
+      e.outh = tp[0].outh;
+      e.h_plane_stride = tp[0].outh ? tp[0].hps : ct.ps;
       e.bias = P(c, base, L.c[CBS]);
       gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.c[CWS]), c->CH1, B, c->CH1,
                               c->S, e);
