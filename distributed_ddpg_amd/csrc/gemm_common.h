@@ -271,7 +271,7 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           if (e.outh)
             store_twin8(e.outh + (size_t)z * e.out_split_stride + o, e.h_plane_stride,
                         e.h_planes, va, vb);
-          if (outp) {
+          if (outp && n >= e.out_col0) {
             *reinterpret_cast<float4*>(outp + o) = va;
             *reinterpret_cast<float4*>(outp + o + 4) = vb;
           }
@@ -286,7 +286,7 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           const float4 v = *reinterpret_cast<const float4*>(Vs + rr * VS_LD + 4 * c4);
           float* o = outp ? outp + (size_t)m * e.ldo + n : nullptr;
           if (e.outh && n < N) store_twin(e, (size_t)z * e.out_split_stride + (size_t)m * e.ldo + n, v);
-          if (!outp) continue;
+          if (!outp || n < e.out_col0) continue;
           if (vst) {
             if (n < N) *reinterpret_cast<float4*>(o) = v;
           } else {

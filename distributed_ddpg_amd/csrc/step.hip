@@ -159,7 +159,7 @@ static Twin critic_l1_parts(ddpg_ctx* c, const float* base, const float* s, cons
   // fp32 values are read only as the action half's EluGrad operand (the
   // action-gradient dX), so the state half writes its twin alone when the
   // hidden layer reads the twin
-  if (!ct.p && cat == c->cat2 && c->hnp == 1 && c->sw.twin_only_cat2) {
+  if (!ct.p && cat == c->cat2 && c->hnp == 1 && c->sw.half_twin) {
     const Twin t2 = act_twin(c, cat);
     if (t2.p && gemm_h_ok<L_RK, L_KR>(c, cat, c->ldC, P(c, base, L.c[CWH]), c->CH2, B, c->CH2,
                                       2 * c->CH1, 1, &kh)) {
@@ -433,6 +433,12 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   e.ldo = c->ldC;
   e.colsum = c->colpart;
   e.ld_colsum = 2 * c->CH1;
+  // one bf16 plane and dWs on the twin GEMM (S > 64, not the skinny kernel):
+  // the state half's fp32 values have no reader -- only the action half
+  // (dWa on the skinny kernel) is stored in fp32
+  if (c->hnp == 1 && c->sw.half_twin && c->S > 64 /* SK_NMAX */ && act_twin(c, c->dcat).p &&
+      gemm_h_ok<L_KR, L_KR>(c, c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, 0, &kh))
+    e.out_col0 = c->CH1;
   GemmPlan pdc = gemm_launch<L_RK, L_RK>(c, "dx", c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]),
                                          c->CH2, B, 2 * c->CH1, c->CH2, e);
   const int mt = pdc.mt(B);

@@ -52,6 +52,9 @@ struct GemmEpi {
   // written (fp32 contexts whose other readers all take the twin)
   const __bf16* auxh;
   long long auxh_ps;
+  // fp32 `out` stored only for columns n >= out_col0 (the twin for all): an
+  // output whose leading columns have twin readers only
+  int out_col0;
 };
 
 struct GemmArgs {

@@ -55,7 +55,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_M
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
-            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_CAT2_TWIN")
+            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN")
 
 
 @pytest.fixture(scope="module")
@@ -210,14 +210,15 @@ def test_gemm_pack_bf16_bitwise(dd, O, monkeypatch):
     _bitwise(got, ref)
 
 
-def test_cat2_twin_only_bf16_bitwise(dd, O, monkeypatch):
-    """bf16 configuration, S = 200: the state half of cat2 (critic at
-    (s, mu)) is written as its bf16 twin only by default -- its fp32 values
-    have no reader -- and in fp32 too with DDPG_CAT2_TWIN=0: bitwise equal."""
+def test_half_twin_bf16_bitwise(dd, O, monkeypatch):
+    """bf16 configuration, S = 200: the state halves of cat2 (critic at
+    (s, mu)) and of dcat (read by dWs through its twin) are stored as bf16
+    twins only by default -- their fp32 values have no reader -- and in fp32
+    too with DDPG_HALF_TWIN=0: bitwise equal."""
     _clear(monkeypatch)
     p, _ = _params(O, "wides")
     ref = _run(dd, O, "wides", p, 2, dtype="bf16")
-    monkeypatch.setenv("DDPG_CAT2_TWIN", "0")
+    monkeypatch.setenv("DDPG_HALF_TWIN", "0")
     got = _run(dd, O, "wides", p, 2, dtype="bf16")
     _bitwise(got, ref)
 
