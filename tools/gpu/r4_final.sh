@@ -22,3 +22,6 @@ sb = d.get("small_batch", {})
 print("C2", sb.get("value"), sb.get("step_latency"))
 print("strong8", d["projected_scaling"]["strong"]["8"]["speedup_vs_1gpu"], "weak8", d["projected_scaling"]["weak"]["8"]["speedup_vs_1gpu"])
 PY
+echo "== DDPG_SLOTS_H2D=1 A/B (slots uploaded vs read in place from pinned host memory)"
+bash tools/gpu/envab.sh DDPG_SLOTS_H2D=1 c3 2 gather 2>&1 | tee gpurun_out/slots_ab_c3.txt
+bash tools/gpu/envab.sh DDPG_SLOTS_H2D=1 c5 2 gather 2>&1 | tee gpurun_out/slots_ab_c5.txt
