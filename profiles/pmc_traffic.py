@@ -36,8 +36,15 @@ def bench_name(rocprof_name):
     if targs is None:
         return sym
     a = [x.strip() for x in targs.split(",")]
+    if sym == "thin_k_kernel" and len(a) == 1:  # MODE: generic / forward / backward form
+        return {"0": "thin_k_kernel", "1": "thin_k_kernel<FWD>", "2": "thin_k_kernel<BWD>"}.get(
+            a[0], "thin_k_kernel<%s>" % a[0])
+    if len(a) < 2:
+        return "%s<%s>" % (sym, a[0])
     lay = {"0": "RK", "1": "KR"}
     a[0], a[1] = lay.get(a[0], a[0]), lay.get(a[1], a[1])
+    if sym == "gemm_h16i_pack_kernel" and len(a) == 2:
+        return "%s<%s,%s,NP=1>" % (sym, a[0], a[1])
     if sym == "gemm_s3_kernel" and len(a) == 3:
         # bench.py labels the one-plane instantiation gemm_bf16_kernel
         return "%s<%s,%s>" % ("gemm_s3_kernel" if a[2] == "3" else "gemm_bf16_kernel", a[0], a[1])
