@@ -168,6 +168,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.tk_fwd = !env_is("DDPG_TK_FWD", "0");
       c->sw.gemm_pack = !env_is("DDPG_GEMM_PACK", "0");
       c->sw.half_twin = !env_is("DDPG_HALF_TWIN", "0");
+      c->sw.skinny_nl = !env_is("DDPG_SKINNY_NL", "0");
       c->sw.prof_shapes = env_is("DDPG_PROF_SHAPES", "1");
       if (const char* v = getenv("DDPG_KCOMB_BLOCKS"))
         c->sw.kc_blocks = std::min(kKcTickets, std::max(1, atoi(v)));

@@ -273,6 +273,7 @@ struct ddpg_ctx {
     bool kcomb = true;       // DDPG_KCOMB=0: no in-launch K split for small-M plain twin GEMMs
     int kc_blocks = 200;     // DDPG_KCOMB_BLOCKS=n: split plain twin GEMMs of fewer tiles
     bool prof_shapes = false;  // DDPG_PROF_SHAPES=1: GEMM / thin_k profile keys carry shapes
+    bool skinny_nl = true;   // DDPG_SKINNY_NL=0: skinny kernel reads narrow rows by scalar loads
     bool half_twin = true;   // DDPG_HALF_TWIN=0: bf16 config stores cat2 / dcat state halves in fp32 too
     bool gemm_pack = true;   // DDPG_GEMM_PACK=0: deferred GEMMs launched one by one
     bool tk_fwd = true;      // DDPG_TK_FWD=0: thin_k's generic epilogue for forward parts too

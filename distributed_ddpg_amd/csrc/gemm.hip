@@ -608,12 +608,24 @@ GemmPlan wgrad_launch(ddpg_ctx* c, const float* A, int lda, const float* B, int 
     }
     ProfScope ps(c, "skinny_wgrad_kernel|wgrad", 2.0 * M * N * (double)K,
                  4.0 * ((double)K * (M + N) + (double)M * N * splits));
-    if (ng == 8)
-      hipLaunchKernelGGL(skinny_wgrad_kernel<8>, dim3(tiles * splits), dim3(SK_NT),
-                         sk_lds_bytes(8), c->cur, a);
-    else
-      hipLaunchKernelGGL(skinny_wgrad_kernel<16>, dim3(tiles * splits), dim3(SK_NT),
-                         sk_lds_bytes(16), c->cur, a);
+    // narrow rows through LDS (skinny.h, NL) when the split's rows fit
+    const bool nl = c->sw.skinny_nl && kc <= sk_nl_rows(ng);
+    const dim3 grid(tiles * splits);
+    if (ng == 8) {
+      if (nl)
+        hipLaunchKernelGGL((skinny_wgrad_kernel<8, SK_R, true>), grid, dim3(SK_NT), sk_lds_bytes(8),
+                           c->cur, a);
+      else
+        hipLaunchKernelGGL((skinny_wgrad_kernel<8, SK_R, false>), grid, dim3(SK_NT),
+                           sk_lds_bytes(8), c->cur, a);
+    } else {
+      if (nl)
+        hipLaunchKernelGGL((skinny_wgrad_kernel<16, SK_R, true>), grid, dim3(SK_NT),
+                           sk_lds_bytes(16), c->cur, a);
+      else
+        hipLaunchKernelGGL((skinny_wgrad_kernel<16, SK_R, false>), grid, dim3(SK_NT),
+                           sk_lds_bytes(16), c->cur, a);
+    }
     HIP_TRY(hipGetLastError());
     return p;
   }
@@ -653,9 +665,13 @@ void gemm_setup(ddpg_ctx* c) {
     HIP_TRY(hipMalloc(&c->kc_ticket, (size_t)c->kc_rot * kKcTickets * sizeof(unsigned)));
     HIP_TRY(hipMemset(c->kc_ticket, 0, (size_t)c->kc_rot * kKcTickets * sizeof(unsigned)));
   }
-  HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<8>,
+  HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<8, SK_R, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, sk_lds_bytes(8)));
-  HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<16>,
+  HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<16, SK_R, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sk_lds_bytes(16)));
+  HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<8, SK_R, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sk_lds_bytes(8)));
+  HIP_TRY(hipFuncSetAttribute((const void*)skinny_wgrad_kernel<16, SK_R, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, sk_lds_bytes(16)));
 }
 

@@ -46,7 +46,14 @@ typedef const __attribute__((address_space(4))) float* sk_const_f;
 
 static_assert(SK_WAVES == 8, "the reduction splits NG = 8 / 16 rows over 8 waves");
 
-template <int NG, int R = SK_R>
+// NL (round 4): the split's narrow rows [b0, b1) x NG are first copied into
+// the reduction's LDS region (coalesced float4 loads by the whole block), and
+// each row's NG values are read from there as broadcast ds_read_b128s, R rows
+// ahead.  The per-row scalar loads of the original form (NL = false) were
+// issued one or two rows ahead at most (the SGPR budget), so every row or two
+// waited a scalar-load round trip.  Same FMAs in the same order: bitwise equal.
+// The host takes NL when (b1 - b0) * NG floats fit the reduction region.
+template <int NG, int R = SK_R, bool NL = false>
 __global__ __launch_bounds__(SK_NT) void skinny_wgrad_kernel(SkArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sk_red[];  // [8][NG * 4][64]
   const int lane = threadIdx.x & 63;
@@ -79,13 +86,36 @@ __global__ __launch_bounds__(SK_NT) void skinny_wgrad_kernel(SkArgs a) {
     for (int u = 0; u < R; ++u)
       w[u] = *reinterpret_cast<const f32x4*>(a.W + (size_t)wrow(r + u) * a.ldw + jc);
   };
+  if constexpr (NL) {
+    // the split's narrow rows -> LDS [b - b0][NG] (the reduction region is
+    // free until the partial tiles are written)
+    constexpr int Q = NG / 4;  // float4 per row
+    f32x4* nl4 = reinterpret_cast<f32x4*>(sk_red);
+    for (int f = threadIdx.x; f < (b1 - b0) * Q; f += SK_NT) {
+      const int rr = f / Q, q = f - rr * Q;
+      nl4[f] = *reinterpret_cast<const f32x4*>(a.N + (size_t)(b0 + rr) * a.ldn + n0 + 4 * q);
+    }
+    __syncthreads();
+  }
   auto row = [&](const f32x4& w, int b) {
-    sk_const_f np = (sk_const_f)(a.N + (size_t)b * a.ldn + n0);
+    if constexpr (NL) {
+      const f32x4* np = reinterpret_cast<const f32x4*>(sk_red) + (size_t)(b - b0) * (NG / 4);
 #pragma unroll
-    for (int i = 0; i < NG; ++i) {
-      const float nv = np[i];
+      for (int q = 0; q < NG / 4; ++q) {
+        const f32x4 nq = np[q];  // same address in every lane: broadcast
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(nv, w[j], acc[i][j]);
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[4 * q + e][j] = fmaf(nq[e], w[j], acc[4 * q + e][j]);
+      }
+    } else {
+      sk_const_f np = (sk_const_f)(a.N + (size_t)b * a.ldn + n0);
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const float nv = np[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(nv, w[j], acc[i][j]);
+      }
     }
   };
   auto step = [&](const f32x4 (&w)[R], int r) {
@@ -114,6 +144,7 @@ __global__ __launch_bounds__(SK_NT) void skinny_wgrad_kernel(SkArgs a) {
   // partial tiles -> LDS; wave wv sums narrow rows wv * IPW .. of the tile
   // over the waves 0 .. 7 in order
   constexpr int E = NG * 4, IPW = NG / SK_WAVES;
+  if constexpr (NL) __syncthreads();  // every wave done with the narrow rows
 #pragma unroll
   for (int i = 0; i < NG; ++i)
 #pragma unroll
@@ -144,5 +175,7 @@ __global__ __launch_bounds__(SK_NT) void skinny_wgrad_kernel(SkArgs a) {
 
 // LDS bytes of the cross-wave reduction
 constexpr int sk_lds_bytes(int ng) { return SK_WAVES * ng * 4 * 64 * 4; }
+// rows of narrow operand the NL form stages (in the same region)
+constexpr int sk_nl_rows(int ng) { return sk_lds_bytes(ng) / (ng * 4); }
 
 }  // namespace ddpg

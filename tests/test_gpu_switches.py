@@ -27,6 +27,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_TK_FWD=0     thin_k's forward and backward parts on the generic epilogue
                       instead of the forward / backward forms (same arithmetic,
                       flags and bounds folded away)
+    DDPG_SKINNY_NL=0  the skinny weight-gradient kernel reads each narrow row by
+                      scalar loads instead of from the split's rows staged in LDS
     DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
                       instead of read in place from the pinned host buffer
   different kernels -- the oracle's fp32 bars (1e-4 after the fused steps):
@@ -55,7 +57,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_M
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
-            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN")
+            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL")
 
 
 @pytest.fixture(scope="module")
@@ -142,6 +144,7 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_GEMM_H3", "0", "wide"),
     ("DDPG_TK_RPB", "3", "wide"),
     ("DDPG_TK_FWD", "0", "wide"),
+    ("DDPG_SKINNY_NL", "0", "wide"),
     ("DDPG_SLOTS_H2D", "1", "wide"),
     ("DDPG_SLOTS_H2D", "1", "ip"),
 ])
