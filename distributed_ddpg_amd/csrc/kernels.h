@@ -189,9 +189,16 @@ __global__ __launch_bounds__(256) void critic_loss_kernel(
 DDPG_DEV void stats_fold(const float2* __restrict__ lpart, int nlp, float inv_b,
                          float* __restrict__ stats, double* __restrict__ acc) {
   float sum = 0.f, mx = -INFINITY;
-  for (int i = 0; i < nlp; ++i) {
-    sum += lpart[i].x;
-    mx = fmaxf(mx, lpart[i].y);
+  for (int i0 = 0; i0 < nlp; i0 += 8) {  // in order, 8 loads in flight
+    float2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = i0 + i < nlp ? lpart[i0 + i] : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i0 + i < nlp) {
+        sum += v[i].x;
+        mx = fmaxf(mx, v[i].y);
+      }
   }
   const float loss = __fmul_rn(sum, inv_b);
   stats[0] = mx;
@@ -234,8 +241,7 @@ __global__ void critic_head_bwd_kernel(const float* __restrict__ h, int ldh,
     part_dbh[(size_t)chunk * H2 + j] = sb;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float s = 0.f;
-    for (int b = b0; b < b1; ++b) s += dq[b];
+    const float s = slab_sum(dq + b0, b1 - b0, 1, 0.f);  // in row order, 8 loads in flight
     part_dbo[chunk] = s;
     if (chunk == 0) stats_fold(lpart, nlp, inv_b, stats, acc);
   }
@@ -319,8 +325,7 @@ __global__ __launch_bounds__(256) void critic_head_bwd4_kernel(
     *reinterpret_cast<float4*>(part_dbh + (size_t)chunk * H2 + j) = sb;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float s = 0.f;
-    for (int b = b0; b < b1; ++b) s += dq[b];
+    const float s = slab_sum(dq + b0, b1 - b0, 1, 0.f);  // in row order, 8 loads in flight
     part_dbo[chunk] = s;
     if (chunk == 0) stats_fold(lpart, nlp, inv_b, stats, acc);
   }
