@@ -696,9 +696,18 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
   SB_STAMP(sbase + 2);
   if (net == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
     float ls = 0.f, qm = -INFINITY;
-    for (int w = 0; w < nslab; ++w) {
-      ls += g.stat_part[2 * w];
-      qm = fmaxf(qm, g.stat_part[2 * w + 1]);
+    for (int w0 = 0; w0 < nslab; w0 += 8) {  // in order, 8 loads in flight
+      f32x2v v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = w0 + u < nslab ? f32x2v{g.stat_part[2 * (w0 + u)], g.stat_part[2 * (w0 + u) + 1]}
+                              : f32x2v{0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (w0 + u < nslab) {
+          ls += v[u][0];
+          qm = fmaxf(qm, v[u][1]);
+        }
     }
     const float loss = __fmul_rn(ls, g.inv_b);
     g.stats[0] = qm;
