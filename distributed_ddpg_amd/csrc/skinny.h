@@ -28,7 +28,10 @@
 
 namespace ddpg {
 
-constexpr int SK_NT = 512, SK_WAVES = 8, SK_WT = 256, SK_NMAX = 64, SK_R = 4;
+#ifndef SK_R_CFG
+#define SK_R_CFG 4  // rows per register set (two sets in flight per wave)
+#endif
+constexpr int SK_NT = 512, SK_WAVES = 8, SK_WT = 256, SK_NMAX = 64, SK_R = SK_R_CFG;
 
 struct SkArgs {
   const float* N;  // narrow operand [B][ldn]: columns 0 .. nn-1 used
