@@ -29,7 +29,7 @@
 namespace ddpg {
 
 #ifndef SK_R_CFG
-#define SK_R_CFG 4  // rows per register set (two sets in flight per wave)
+#define SK_R_CFG 6  // rows per register set (two sets in flight per wave; 4 -> 6: +0.4 % C3)
 #endif
 constexpr int SK_NT = 512, SK_WAVES = 8, SK_WT = 256, SK_NMAX = 64, SK_R = SK_R_CFG;
 
