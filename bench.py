@@ -683,6 +683,7 @@ def main():
         ms5 = 1000.0 * el5 / 30
         ach5 = (d5["flops"] / d5["launches"]) / (d5["ms"] / d5["launches"] * 1e-3) / 1e12
         pk5 = kernel_peak(dn5)
+        tr5, tr5_src = pmc_traffic("c5", dn5, d5["launches"] / 10) if world == 1 else (None, None)
         out["c5_bf16"] = {
             "workload": label5 + ", bf16 GEMM operands (fp32 master weights/accumulation)",
             "value": round((1 if strong else world) * 30 / el5, 3), "unit": "updates/s",
@@ -693,7 +694,8 @@ def main():
             "mfma_util_step": round(f5 / (ms5 * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS, 4),
             "mfma_busy_step_counter": mfma_busy_step("c5", ms5) if world == 1 else None,
             "roofline": {"bound": "mfma", "kernel": dn5, "achieved": round(ach5, 2), "peak": pk5,
-                         "unit": "TFLOP/s", "frac": round(ach5 / pk5, 4),
+                         "unit": "TFLOP/s", "frac": round(ach5 / pk5, 4), "traffic": tr5,
+                         "traffic_source": tr5_src,
                          "avg_launch_us": round(1e3 * d5["ms"] / d5["launches"], 2),
                          "launches_per_step": d5["launches"] / 10},
             "kernels": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
