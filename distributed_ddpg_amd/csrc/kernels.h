@@ -29,18 +29,10 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  // the block's first rows' slots in one coalesced read (the slots may be in
-  // pinned host memory: one PCIe request per block instead of one per wave)
-  __shared__ int s_slot[8];
-  const int wpb = blockDim.x >> 6, b_first = blockIdx.x * wpb;
-  if (threadIdx.x < wpb && threadIdx.x < 8 && b_first + (int)threadIdx.x < B)
-    s_slot[threadIdx.x] = slots[b_first + threadIdx.x];
-  __syncthreads();
   // fp32 ring with 4-aligned rows: 16-B accesses (4 features per lane)
   const bool v4 = !rsd && (S & 3) == 0 && (lds & 3) == 0 && (hps & 3) == 0;
   for (int b = wave; b < B; b += nwaves) {
-    const int wl = b - b_first;
-    const size_t slot = (size_t)(wl >= 0 && wl < wpb && wl < 8 ? s_slot[wl] : slots[b]);
+    const size_t slot = (size_t)slots[b];
     if (v4) {
       for (int j = 4 * lane; j < S; j += 256) {
         const size_t e = slot * S + j;
