@@ -43,9 +43,14 @@ DDPG_DEV int tk_swz(int r) { return (r >> 1) & 7; }
 #define TK_LANDED(x) asm volatile("" ::"v"(x))
 DDPG_DEV int tk_off(int r, int k) { return r * 128 + 16 * ((k >> 3) ^ tk_swz(r)) + 2 * (k & 7); }
 // output tile: float (r, n) -- the MFMA write of lanes h = 0 / 1 (rows r, r + 4)
-// lands in opposite 128-B halves of the banks
+// lands in opposite 128-B halves of the banks; the quad's low bit is XORed
+// with bit 4 of the quad index, so the epilogue's 8-column row reads (quads
+// 2 c8 and 2 c8 + 1, lanes of a ds_read_b128 group spanning c8 and c8 + 8)
+// hit 16 distinct 16-B bank slots instead of 8 twice (SQ_LDS_BANK_CONFLICT
+// was 16-23 % of thin_k's LDS cycles, profiles/r4/lds_conflicts.txt)
 DDPG_DEV int tk_oidx(int r, int n) {
-  return r * TK_COLS + (((n >> 2) ^ (((r >> 2) & 1) << 3)) << 2) + (n & 3);
+  const int q = n >> 2;
+  return r * TK_COLS + ((q ^ (((r >> 2) & 1) << 3) ^ ((q >> 4) & 1)) << 2) + (n & 3);
 }
 
 // Block (column block x, row tiles [rpb y, rpb y + rpb), part z): the W panel
