@@ -117,7 +117,6 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       HIP_TRY(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor,
                                     k.device));
       c->tk_slots = std::max(1, cus) * std::max(1, lds / TK_LDS);
-      c->tkp_slots = std::max(1, cus) * std::max(1, lds / (3 * TK_WIMG + 2 * TK_XREG));
     }
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->cur = c->stream;
@@ -170,7 +169,6 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_pack = !env_is("DDPG_GEMM_PACK", "0");
       c->sw.half_twin = !env_is("DDPG_HALF_TWIN", "0");
       c->sw.skinny_nl = !env_is("DDPG_SKINNY_NL", "0");
-      c->sw.tk_pipe = env_is("DDPG_TK_PIPE", "1");
       c->sw.prof_shapes = env_is("DDPG_PROF_SHAPES", "1");
       if (const char* v = getenv("DDPG_KCOMB_BLOCKS"))
         c->sw.kc_blocks = std::min(kKcTickets, std::max(1, atoi(v)));

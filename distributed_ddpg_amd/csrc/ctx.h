@@ -273,7 +273,6 @@ struct ddpg_ctx {
     bool kcomb = true;       // DDPG_KCOMB=0: no in-launch K split for small-M plain twin GEMMs
     int kc_blocks = 200;     // DDPG_KCOMB_BLOCKS=n: split plain twin GEMMs of fewer tiles
     bool prof_shapes = false;  // DDPG_PROF_SHAPES=1: GEMM / thin_k profile keys carry shapes
-    bool tk_pipe = false;    // DDPG_TK_PIPE=1: forward thin_k parts on the phase-offset 8-wave kernel
     bool skinny_nl = true;   // DDPG_SKINNY_NL=0: skinny kernel reads narrow rows by scalar loads
     bool half_twin = true;   // DDPG_HALF_TWIN=0: bf16 config stores cat2 / dcat state halves in fp32 too
     bool gemm_pack = true;   // DDPG_GEMM_PACK=0: deferred GEMMs launched one by one
@@ -291,7 +290,6 @@ struct ddpg_ctx {
   int kc_rot = 0, kc_next = 0;
   int gemm_defer = 0;  // > 0: gemm_launch queues gemm_h16i GEMMs for gemm_flush
   std::vector<DeferredGemm> deferred;
-  int tkp_slots = 256;  // thin_k_pipe_kernel blocks resident at once
   int tk_slots = 512;  // thin_k blocks resident at once (ddpg_create: CUs x blocks per CU)
 
   // comm: every collective of the ctx is issued on cs (one stream, so the

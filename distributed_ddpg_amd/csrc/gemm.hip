@@ -527,6 +527,14 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
   // CU's LDS holds -- 256 x 2 on MI355X), so that a block stages its W panel
   // once for several row tiles and overlaps the next X tile's loads with its
   // stores (env DDPG_TK_RPB=n forces n; 1 = one tile)
+  int rpb = 1;
+  if (c->sw.tk_rpb > 0) {
+    rpb = std::min(c->sw.tk_rpb, mt);
+  } else {
+    while (rpb < mt && nc * nparts * ceil_div(mt, rpb) > c->tk_slots) ++rpb;
+  }
+  a.mt = mt;
+  a.rpb = rpb;
   // the forward / backward forms when every part is one (thin_k.h)
   bool fwd = c->sw.tk_fwd && M % TK_ROWS == 0, bwd = fwd;
   for (int i = 0; i < nparts; ++i) {
@@ -536,33 +544,14 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
     fwd = fwd && full && q.bias && q.act == 1 && q.outh && !q.aux && !q.colsum;
     bwd = bwd && full && !q.bias && q.act == 0 && q.aux && q.colsum && q.ldaux % 4 == 0;
   }
-  const bool pipe = fwd && c->sw.tk_pipe;
-  // row tiles per block: the fewest that keep the grid within one round of
-  // the device's block slots (tk_slots: CUs x the TK_LDS-byte blocks one
-  // CU's LDS holds -- 256 x 2 on MI355X; the pipe kernel: one 8-wave block
-  // per CU, at least two tiles so both its groups work), so that a block
-  // stages its W panel once for several row tiles and overlaps the next X
-  // tile's loads with its stores (env DDPG_TK_RPB=n forces n; 1 = one tile)
-  int rpb = pipe ? std::min(2, mt) : 1;
-  if (c->sw.tk_rpb > 0) {
-    rpb = std::min(c->sw.tk_rpb, mt);
-  } else {
-    const int slots = pipe ? c->tkp_slots : c->tk_slots;
-    while (rpb < mt && nc * nparts * ceil_div(mt, rpb) > slots) ++rpb;
-  }
-  a.mt = mt;
-  a.rpb = rpb;
   char key[96];
-  snprintf(key, sizeof key, "thin_k_%s%s|%s", pipe ? "pipe_kernel" : "kernel",
-           fwd ? "<FWD>" : bwd ? "<BWD>" : "", name);
+  snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : bwd ? "<BWD>" : "", name);
   if (c->sw.prof_shapes)
     snprintf(key + strlen(key), sizeof key - strlen(key), " %dp %dx%dx%d", nparts, M, parts[0].N,
              parts[0].K);
   ProfScope ps(c, key, flops, bytes);
   const dim3 grid(nc, ceil_div(mt, rpb), nparts);
-  if (pipe)
-    hipLaunchKernelGGL(thin_k_pipe_kernel, grid, dim3(TKP_NT), 0, c->cur, a);
-  else if (fwd)
+  if (fwd)
     hipLaunchKernelGGL(thin_k_kernel<1>, grid, dim3(TK_NT), 0, c->cur, a);
   else if (bwd)
     hipLaunchKernelGGL(thin_k_kernel<2>, grid, dim3(TK_NT), 0, c->cur, a);

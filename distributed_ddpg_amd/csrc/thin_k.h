@@ -300,180 +300,4 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   }
 }
 
-// Forward form (MODE 1 semantics) on 8-wave blocks, two 4-wave groups with
-// their phases offset (round 4).  Both groups share the W image; each has its
-// own X image / output tile and walks alternate row tiles of the block.  A
-// tile takes four phases -- 0 X split into the image, 1 MFMAs, 2 accumulators
-// -> output tile, 3 epilogue row loop and stores -- separated by block-wide
-// barriers; group 1 runs two phases behind group 0, so one group's MFMAs
-// overlap the other's VALU-bound epilogue (at two independent 4-wave blocks
-// per CU the phases lined up by chance).  Same arithmetic per output as
-// thin_k_kernel<1>: bitwise equal.
-constexpr int TKP_NT = 2 * TK_NT;
-constexpr int TKP_LDS = 3 * TK_WIMG + 2 * TK_XREG;
-
-__global__ __launch_bounds__(TKP_NT) void thin_k_pipe_kernel(TkArgs args) {
-  __shared__ __attribute__((aligned(16))) char lds[TKP_LDS];
-  char* const wimg = lds;
-  const TkPart P = args.p[blockIdx.z];
-  const int g = threadIdx.x / TK_NT;  // group
-  const int tid = threadIdx.x % TK_NT, wave = tid >> 6, lane = tid & 63;
-  char* const ximg = lds + 3 * TK_WIMG + g * TK_XREG;
-  float* const Os = reinterpret_cast<float*>(ximg);
-  const int li = lane & 31, h = lane >> 5;
-  const int wr = wave & 1, wc = wave >> 1;
-  const int n0 = blockIdx.x * TK_COLS;
-  const int rt0 = blockIdx.y * args.rpb, rt1 = min(args.mt, rt0 + args.rpb);
-  if (n0 >= P.N || rt0 >= rt1) return;  // block-uniform
-  const int K = P.K;
-  const int KS = (K + 15) >> 4;
-  const int KP = 16 * KS;
-  f32x4 xg[4];
-  auto load_x = [&](int rt) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = tid + TK_NT * j, r = f >> 4, k = 4 * (f & 15), m = rt * TK_ROWS + r;
-      xg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (k < K) xg[j] = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + k);
-    }
-  };
-  auto put4 = [&](char* img, int plane_bytes, int r, int k, f32x4 v) {
-    bf16x2 h0, m0_, l0, h1, m1, l1;
-    split3_pair(f32x2v{v[0], v[1]}, h0, m0_, l0);
-    split3_pair(f32x2v{v[2], v[3]}, h1, m1, l1);
-    const int off = tk_off(r, k);
-    *reinterpret_cast<bf16x4*>(img + off) = bf16x4{h0[0], h0[1], h1[0], h1[1]};
-    *reinterpret_cast<bf16x4*>(img + plane_bytes + off) = bf16x4{m0_[0], m0_[1], m1[0], m1[1]};
-    *reinterpret_cast<bf16x4*>(img + 2 * plane_bytes + off) = bf16x4{l0[0], l0[1], l1[0], l1[1]};
-  };
-  // this group's tiles: rt0 + g, rt0 + g + 2, ...
-  const int ntile = rt1 - rt0;
-  const int ng = (ntile - g + 1) / 2;  // tiles of this group (0 when g > ntile - 1)
-  if (ng > 0) load_x(rt0 + g);
-  if (g == 0) {  // W panel: group 0 loads and splits it once
-    const int wcol = tid % TK_COLS, kq = tid / TK_COLS, wn = n0 + wcol;
-    f32x4 wv[TK_WJ];
-    const bool wvec = P.w_nk && ((P.ldw & 3) == 0) && (((uintptr_t)P.W & 15) == 0);
-    const int wnc = min(wn, P.N - 1);
-    if (wvec) {
-#pragma unroll
-      for (int j = 0; j < TK_WJ; ++j) {
-        const int k = 4 * (kq + TK_KQS * j);
-        wv[j] = *reinterpret_cast<const f32x4*>(P.W + (size_t)wnc * P.ldw + min(k, K - 4));
-      }
-    } else if (P.w_nk) {
-#pragma unroll
-      for (int j = 0; j < TK_WJ; ++j) {
-        const float* q = P.W + (size_t)wnc * P.ldw + min(4 * (kq + TK_KQS * j), K - 4);
-        wv[j] = f32x4{q[0], q[1], q[2], q[3]};
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < TK_WJ; ++j) {
-        const int k = min(4 * (kq + TK_KQS * j), K - 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) wv[j][e] = P.W[(size_t)(k + e) * P.ldw + wnc];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TK_WJ; ++j)
-      if (4 * (kq + TK_KQS * j) >= K || wn >= P.N) wv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < TK_WJ; ++j) {
-      const int k = 4 * (kq + TK_KQS * j);
-      if (k < KP) put4(wimg, TK_WIMG, wcol, k, wv[j]);
-    }
-  }
-  const int c8 = tid % TK_OCT, rg = tid / TK_OCT, n = n0 + 8 * c8;
-  const f32x4 bq0 = *reinterpret_cast<const f32x4*>(P.bias + n);
-  const f32x4 bq1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
-  TK_LANDED(bq0);
-  TK_LANDED(bq1);
-  const int ra = 32 * wr + li;
-  f32x16 acc[TK_TPW], acs[TK_TPW];
-  __syncthreads();  // W image complete
-  // steps: group g runs phase (s - 2 g) of its tile sequence; every thread
-  // passes the same barriers
-  const int nsteps = 4 * ((ntile + 1) / 2) + 2;
-  for (int st = 0; st < nsteps; ++st) {
-    const int ph = st - 2 * g;
-    const int j = ph >> 2, p = ph & 3;
-    if (ph >= 0 && j < ng) {
-      const int rt = rt0 + g + 2 * j;
-      if (p == 0) {  // X tile -> image
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int f = tid + TK_NT * q, r = f >> 4, k = 4 * (f & 15);
-          if (k < KP) put4(ximg, TK_XIMG, r, k, xg[q]);
-        }
-      } else if (p == 1) {  // MFMAs; the group's next X tile in flight
-        if (j + 1 < ng) load_x(rt + 2);
-#pragma unroll
-        for (int t = 0; t < TK_TPW; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[t][r] = acs[t][r] = 0.f;
-        for (int ks = 0; ks < KS; ++ks) {
-          const int kk = 16 * ks + 8 * h;
-          bf16x8 a[3], b[TK_TPW][3];
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) {
-            a[pl] = *reinterpret_cast<const bf16x8*>(ximg + pl * TK_XIMG + tk_off(ra, kk));
-#pragma unroll
-            for (int t = 0; t < TK_TPW; ++t)
-              b[t][pl] = *reinterpret_cast<const bf16x8*>(
-                  wimg + pl * TK_WIMG + tk_off((TK_COLS / 2) * wc + 32 * t + li, kk));
-          }
-#pragma unroll
-          for (int t = 0; t < TK_TPW; ++t) {
-            f32x16 q = acs[t];
-            q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[t][0], q, 0, 0, 0);
-            q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][1], q, 0, 0, 0);
-            q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][2], q, 0, 0, 0);
-            q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[t][0], q, 0, 0, 0);
-            q = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][1], q, 0, 0, 0);
-            acs[t] = q;
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[t][0], acc[t], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < TK_TPW; ++t) acc[t] += acs[t];
-      } else if (p == 2) {  // accumulators -> output tile (the X image is free)
-        // the next X tile's loads land here, before this tile's epilogue stores
-        // are issued (a wait for them after the stores would drain the stores)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) TK_LANDED(xg[q]);
-        const int rb = 32 * wr + 4 * h;
-#pragma unroll
-        for (int t = 0; t < TK_TPW; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            Os[tk_oidx(rb + (r & 3) + 8 * (r >> 2), (TK_COLS / 2) * wc + 32 * t + li)] = acc[t][r];
-      } else {  // epilogue: rows of 8 columns, bias, elu, fp32 copy, twin
-        const int m0 = rt * TK_ROWS;
-        constexpr int RPT = TK_ROWS / TK_RG;
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-          const int rl = rg + TK_RG * i, m = m0 + rl;
-          f32x4 v[2];
-          v[0] = *reinterpret_cast<const f32x4*>(Os + tk_oidx(rl, 8 * c8));
-          v[1] = *reinterpret_cast<const f32x4*>(Os + tk_oidx(rl, 8 * c8 + 4));
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              v[u][e] = elu_f(__fadd_rn(v[u][e], u ? bq1[e] : bq0[e]));
-          const size_t o = (size_t)m * P.ldo + n;
-          if (P.out) {
-            *reinterpret_cast<f32x4*>(P.out + o) = v[0];
-            *reinterpret_cast<f32x4*>(P.out + o + 4) = v[1];
-          }
-          store_twin8(P.outh + o, P.hps, P.hnp, make_float4(v[0][0], v[0][1], v[0][2], v[0][3]),
-                      make_float4(v[1][0], v[1][1], v[1][2], v[1][3]));
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
 }  // namespace ddpg

@@ -27,8 +27,6 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_TK_FWD=0     thin_k's forward and backward parts on the generic epilogue
                       instead of the forward / backward forms (same arithmetic,
                       flags and bounds folded away)
-    DDPG_TK_PIPE=1    thin_k's forward parts on the 8-wave kernel whose two groups
-                      run with offset phases (same arithmetic per output)
     DDPG_SKINNY_NL=0  the skinny weight-gradient kernel reads each narrow row by
                       scalar loads instead of from the split's rows staged in LDS
     DDPG_SLOTS_H2D=1  the step's replay slots uploaded to device memory first
@@ -59,8 +57,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_M
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
-            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
-            "DDPG_TK_PIPE")
+            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL")
 
 
 @pytest.fixture(scope="module")
@@ -148,7 +145,6 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_TK_RPB", "3", "wide"),
     ("DDPG_TK_FWD", "0", "wide"),
     ("DDPG_SKINNY_NL", "0", "wide"),
-    ("DDPG_TK_PIPE", "1", "wide"),
     ("DDPG_SLOTS_H2D", "1", "wide"),
     ("DDPG_SLOTS_H2D", "1", "ip"),
 ])
@@ -214,18 +210,6 @@ def test_gemm_pack_bf16_bitwise(dd, O, monkeypatch):
     monkeypatch.setenv("DDPG_GEMM_PACK", "0")
     got = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
     assert not any(k.startswith("gemm_h16i_pack_kernel") for k in got["keys"]), got["keys"]
-    _bitwise(got, ref)
-
-
-def test_tk_pipe_bf16_bitwise(dd, O, monkeypatch):
-    """bf16 configuration: thin_k's forward parts on thin_k_pipe_kernel
-    (DDPG_TK_PIPE=1) against the 4-wave forward form -- bitwise."""
-    _clear(monkeypatch)
-    p, _ = _params(O, "wide")
-    ref = _run(dd, O, "wide", p, 2, dtype="bf16")
-    monkeypatch.setenv("DDPG_TK_PIPE", "1")
-    got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
-    assert any(k.startswith("thin_k_pipe_kernel") for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 
