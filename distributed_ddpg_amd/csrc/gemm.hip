@@ -263,6 +263,7 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
         const int tiles = h.nt(N) * h.mt(M);
         const int nkt = Kh / BKh;
         int sk = std::min({ceil_div(256, tiles), nkt / 3, c->sw.kc_splits});
+        while (sk > 2 && (size_t)sk * tiles * BMh * HG_BN > c->kc_part_n) --sk;  // partial buffer
         if (tiles < c->sw.kc_blocks && sk >= 2) {
           const int kps = ceil_div(nkt, sk) * BKh;
           sk = ceil_div(Kh, kps);

@@ -409,30 +409,42 @@ DDPG_DEV bool ksplit_combine(f32x16* acc, float* part, unsigned* ticket, int til
                    rs, zz * slab + (unsigned)(((v * 4 + q) * nt + tid) * 16), 0, KC_SC1));
   };
   if constexpr (NV <= 2) {
-    // every other split's partial in flight at once (one memory round trip,
-    // not S - 1 of them): slot j holds split j + (j >= z); then the sum in
-    // split order 0 .. S-1 (the host caps S at KC_MAXS)
-    f32x4 x[KC_MAXS - 1][NV][4];
+    // the other splits' partials in flight four at a time (one memory round
+    // trip per four splits, not one per split), summed in split order 0 ..
+    // S-1 (own partial from the registers); the host caps S at KC_MAXS
+    f32x4 t[NV][4];
 #pragma unroll
-    for (int j = 0; j < KC_MAXS - 1; ++j) {
-      const int zz = j + (j >= z);
+    for (int c0 = 0; c0 < KC_MAXS; c0 += 4) {
+      if (c0 >= S) break;
+      f32x4 x[4][NV][4];
 #pragma unroll
-      for (int v = 0; v < NV; ++v)
+      for (int j = 0; j < 4; ++j) {
+        const int zz = c0 + j;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[j][v][q] = zz < S ? ld(zz, v, q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            x[j][v][q] = zz < S && zz != z
+                             ? ld(zz, v, q)
+                             : f32x4{acc[v][4 * q], acc[v][4 * q + 1], acc[v][4 * q + 2],
+                                     acc[v][4 * q + 3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int zz = c0 + j;
+        if (zz < S)
+#pragma unroll
+          for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[v][q] = zz == 0 ? x[j][v][q] : t[v][q] + x[j][v][q];
+      }
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 own{acc[v][4 * q], acc[v][4 * q + 1], acc[v][4 * q + 2], acc[v][4 * q + 3]};
-        f32x4 t = z == 0 ? own : x[0][v][q];
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int zz = 1; zz < KC_MAXS; ++zz)
-          if (zz < S) t += zz == z ? own : zz < z ? x[zz][v][q] : x[zz - 1][v][q];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[v][4 * q + e] = t[e];
-      }
+        for (int e = 0; e < 4; ++e) acc[v][4 * q + e] = t[v][q][e];
   } else {
     // 256-row tiles (64 accumulators per lane): no registers for S - 1
     // partials at once -- one split per round trip, in split order

@@ -12,8 +12,8 @@ namespace ddpg {
 enum { L_RK = 0, L_KR = 1 };
 
 // in-launch K split (ksplit_combine, gemm_common.h): at most KC_MAXS splits
-// per tile -- the partials the last block holds in registers at once
-constexpr int KC_MAXS = 4;
+// per tile (the host's default cap is 4, DDPG_KCOMB_SPLITS up to KC_MAXS)
+constexpr int KC_MAXS = 8;
 constexpr int GBK = 32, GNT = 256;
 constexpr int PROJ_MAX = 32;
 
