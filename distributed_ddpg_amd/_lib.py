@@ -109,6 +109,7 @@ PROTOTYPES = [
     ("ddpg_comm_unique_id", _c.c_int, [_c.c_char_p]),
     ("ddpg_comm_init", _c.c_int, [_P, _c.c_char_p, _c.c_int, _c.c_int]),
     ("ddpg_comm_init_proxy", _c.c_int, [_P]),
+    ("ddpg_step_counts", _c.c_int, [_P, _i64p, _i64p, _c.POINTER(_c.c_int)]),
     ("ddpg_profile_enable", _c.c_int, [_P, _c.c_int]),
     ("ddpg_profile_read", _c.c_int, [_P, _c.c_int, _P, _dp, _i64p, _dp, _dp]),
     ("ddpg_crc32c", _c.c_uint32, [_c.c_uint32, _c.c_void_p, _c.c_size_t]),

@@ -156,6 +156,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
       c->sw.gemm_h3 = !env_is("DDPG_GEMM_H3", "0");
+      c->sw.gemm_m16 = !env_is("DDPG_GEMM_M16", "0");
       if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = atoi(v) == 1;
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
@@ -431,6 +432,15 @@ int ddpg_read_stats(ddpg_ctx* c, double* qsum, double* lsum, int64_t* steps, int
     if (lsum) *lsum = acc[1];
     if (steps) *steps = (int64_t)acc[2];
     if (reset) HIP_TRY(hipMemsetAsync(c->dacc, 0, 4 * sizeof(double), c->stream));
+  });
+}
+
+// ---------------------------------------------------------------- step mode
+int ddpg_step_counts(ddpg_ctx* c, int64_t* graphed, int64_t* eager, int* capture_failed) {
+  return guard(c, [&] {
+    if (graphed) *graphed = c->n_graph_steps;
+    if (eager) *eager = c->n_eager_steps;
+    if (capture_failed) *capture_failed = c->graph_fail;
   });
 }
 

@@ -262,6 +262,7 @@ struct ddpg_ctx {
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
     bool gemm_h3 = true;   // DDPG_GEMM_H3=0: twin GEMMs with runtime slot addressing (gemm_h_kernel / gemm_h16_kernel)
+    bool gemm_m16 = true;  // DDPG_GEMM_M16=0: fp32 contexts on the 32x32x16 gemm_h3_kernel instead of gemm_h3m_kernel
     int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h (opt-in)
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
@@ -301,6 +302,9 @@ struct ddpg_ctx {
   // the step graph captures the collectives too (env DDPG_GRAPH_COMM=0: such
   // steps stay eager); cleared if a capture with RCCL calls fails
   bool comm_graph = true;
+  // learner steps run as a graph replay / eagerly (ddpg_step_counts)
+  long long n_graph_steps = 0, n_eager_steps = 0;
+  int graph_fail = 0;  // a capture with RCCL calls failed on this ctx
   hipStream_t cs = nullptr;
   hipEvent_t cev[8] = {};
   int win_rec = -1;     // profiling: open exchange-overlap window (prof_recs index)

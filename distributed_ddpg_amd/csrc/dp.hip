@@ -80,12 +80,18 @@ void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0
   }
   {
     ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0 + (with_stats ? 8.0 * c->cworld : 0.0));
+    // the group is closed on every path: a call that fails inside it still
+    // runs ncclGroupEnd before the error propagates, so the thread's group
+    // depth is back to zero for the caller's next (eager) step
     nccl_try(ncclGroupStart());
-    if (n0) nccl_try(ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs));
-    if (n1) nccl_try(ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs));
-    if (with_stats)
-      nccl_try(ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs));
-    nccl_try(ncclGroupEnd());
+    ncclResult_t r = ncclSuccess;
+    if (n0) r = ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs);
+    if (r == ncclSuccess && n1) r = ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs);
+    if (r == ncclSuccess && with_stats)
+      r = ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs);
+    const ncclResult_t re = ncclGroupEnd();
+    nccl_try(r);
+    nccl_try(re);
   }
   c->cur = prev;
 }

@@ -8,7 +8,7 @@
 #include "gemm_s3.h"
 #include "gemm_h.h"
 #include "gemm_h256.h"
-#include "gemm_h3.h"
+#include "gemm_h3m.h"
 #include "thin_k.h"
 #include "skinny.h"
 
@@ -320,6 +320,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       }
       // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
       const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
+      // fp32 contexts: RK-A GEMMs (forward, dX) on the 16x16x32 form
+      const bool m16 = c->hnp == 3 && AL == L_RK && c->sw.gemm_m16;
       char key[112];
       // "/kc": the splits are combined in-launch (small-M plan)
       // DDPG_PROF_SHAPES=1: the shape and split count in the key too
@@ -327,7 +329,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       if (c->sw.prof_shapes) snprintf(shp, sizeof shp, " %dx%dx%d/%d", M, N, K, h.splits);
       snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s%s%s",
                h16 ? (AL == L_RK && c->sw.gemm_h3 ? "gemm_h16i_kernel" : "gemm_h16_kernel")
-                   : (c->hnp == 3 && c->sw.gemm_h3) ? "gemm_h3_kernel" : "gemm_h_kernel",
+                   : (c->hnp == 3 && c->sw.gemm_h3) ? (m16 ? "gemm_h3m_kernel" : "gemm_h3_kernel")
+                                                    : "gemm_h_kernel",
                lay[AL], lay[BL], c->hnp, name, a.kpart ? "/kc" : "", shp);
       const dim3 grid(h.nt(N), h.mt(M), h.splits);
       const double fl = 2.0 * M * N * (double)K,
@@ -354,7 +357,11 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
         hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else if (c->hnp == 1)
         hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
-      else if (c->sw.gemm_h3)
+      else if (c->sw.gemm_h3 && m16) {
+        // the same six plane products on the 16x16x32 MFMA (gemm_h3m.h), RK A operands
+        if constexpr (AL == L_RK)
+          hipLaunchKernelGGL((gemm_h3m_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
+      } else if (c->sw.gemm_h3)
         // the same kernel with immediate-offset addressing (gemm_h3.h)
         hipLaunchKernelGGL((gemm_h3_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
       else

@@ -30,7 +30,14 @@
 namespace ddpg {
 
 template <int AL, int BL>
-#ifdef DDPG_KC_STAMPS  // tools/kc_bench.hip: s_memrealtime per phase, lane 0 of each block
+#if defined(DDPG_KC_STAMPS) && defined(DDPG_STAMPS8)  // tools/h3_phase_bench.hip: + shader clock
+#define KC_STAMP(i)                                                                    \
+  if (g.stamps && threadIdx.x == 0) {                                                  \
+    const unsigned b_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+    g.stamps[b_ * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                         \
+    g.stamps[b_ * 8 + 4 + (i)] = __builtin_amdgcn_s_memtime();                         \
+  }
+#elif defined(DDPG_KC_STAMPS)  // tools/kc_bench.hip: s_memrealtime per phase, lane 0 of each block
 #define KC_STAMP(i)                                                                    \
   if (g.stamps && threadIdx.x == 0)                                                    \
     g.stamps[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (i)] = \
@@ -88,6 +95,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
   // DMA piece q of k-tile t into slot SL: q = 2 p + (0: A, 1: B)
   auto piece = [&](int t, auto sl_c, int q) {
     constexpr int SL = decltype(sl_c)::value;
+#ifdef DDPG_H3_ABL_NODMA  // tools/h3_phase_bench.hip ablation only: no staging after the prologue
+    if (t > 1) return;
+#endif
     const int p = q >> 1;
     if ((q & 1) == 0)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -139,6 +149,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
     constexpr int P = J / (TM + TN), F = J % (TM + TN);
     constexpr int REG = SL == 2 ? 1 : 0;
     constexpr int SO = SL == 2 ? 0 : SL;  // slot within the region
+#ifdef DDPG_H3_ABL_NOREAD  // tools/h3_phase_bench.hip ablation only
+    return;
+#endif
     if constexpr (F < TN) {
       constexpr int OFF = SO * BSLOT + P * C::B_BYTES;
       if constexpr (BL == L_RK) {
@@ -164,6 +177,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
   };
   // the 6 plane products of output block i, in gemm_h_kernel's order
   auto mfma_q = [&](int i, int q, bf16x8 (&av)[NP][TM], bf16x8 (&bv)[NP][TN]) {
+#ifdef DDPG_H3_ABL_NOMFMA  // tools/h3_phase_bench.hip ablation only
+    return;
+#endif
     if (q == 0) acs[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][0], acs[i][0], 0, 0, 0);
     if (q == 1) acs[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][0], acs[i][0], 0, 0, 0);
     if (q == 2) acs[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][0], acs[i][0], 0, 0, 0);
@@ -244,6 +260,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
     asm volatile("" ::: "memory");
     static_for<NRG>([&](auto j_c) { read_one(S0{}, std::integral_constant<int, 0>{}, j_c, fa[0], fb[0]); });
     __builtin_amdgcn_sched_barrier(0);
+#ifdef DDPG_H3_STAMP_PROLOGUE
+    KC_STAMP(2)
+#endif
     int t = 0;
     // full trips of three tiles (slots 0, 1, 2), each staging t + 2
     for (; t + 4 < nk; t += 3) {
@@ -284,7 +303,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
       return;
     ze = 0;
   }
+#ifndef DDPG_H3_STAMP_PROLOGUE
   KC_STAMP(2)
+#endif
   __syncthreads();  // staging buffers are reused by the epilogue
   GemmArgs ge;
   ge.M = g.M;

@@ -1149,8 +1149,13 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
         g.exec = nullptr;
         (void)hipGetLastError();
         if (!c->comm) throw;
-        // RCCL calls did not capture here: this ctx runs its steps eagerly
+        // RCCL calls did not capture here: this ctx runs its steps eagerly.
+        // The failed capture launched nothing (its collectives were only
+        // recorded) and allreduce_on_cs closed its group, so the eager step
+        // below issues the same collectives in the same order as a peer rank
+        // replaying its graph.  Visible through ddpg_step_counts.
         c->comm_graph = false;
+        c->graph_fail = 1;
         c->cur = c->stream;
         c->td_nqt = 0;
         fprintf(stderr, "[ddpg] step graph with RCCL calls failed (%s); eager steps\n",
@@ -1167,6 +1172,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
       HIP_TRY(hipGraphLaunch(g.exec, c->stream));
       HIP_TRY(hipEventRecord(g.done, c->stream));
       graphed = true;
+      ++c->n_graph_steps;
     }
   }
   if (!graphed) {
@@ -1190,6 +1196,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     }
     c->slots_src = nullptr;
     HIP_TRY(hipEventRecord(c->slot_ev[si], c->stream));
+    ++c->n_eager_steps;
   }
   HIP_TRY(hipEventRecord(rb->last_read, c->stream));
   HIP_TRY(hipEventRecord(c->step_done, c->stream));

@@ -71,11 +71,23 @@ class FusedLearner:
             return self._stats.q_max, self._stats.loss
         return None
 
+    def step_counts(self):
+        """(graph-replayed steps, eager steps, capture_failed) of this context
+        so far (ddpg_step_counts)."""
+        return step_counts(self.sess)
+
     def read_stats(self, reset=True):
         q, l, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         check(lib.ddpg_read_stats(self.sess.ctx, ctypes.byref(q), ctypes.byref(l),
                                   ctypes.byref(n), int(reset)), self.sess.ctx)
         return q.value, l.value, n.value
+
+
+def step_counts(sess):
+    g, e, f = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+    check(lib.ddpg_step_counts(sess.ctx, ctypes.byref(g), ctypes.byref(e), ctypes.byref(f)),
+          sess.ctx)
+    return g.value, e.value, bool(f.value)
 
 
 def fill_synthetic(replay, s_dim, a_dim, n, scale=1.0, seed=0, chunk=65536):

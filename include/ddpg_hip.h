@@ -227,6 +227,11 @@ int ddpg_comm_init(ddpg_ctx* ctx, const char* id128, int world, int rank);
  * then this rank's partial sums, not the global ones. */
 int ddpg_comm_init_proxy(ddpg_ctx* ctx);
 
+/* How this ctx's learner steps ran so far: replayed from the step's hipGraph
+ * or launched eagerly, and whether a capture with RCCL calls failed (the ctx
+ * then runs its data-parallel steps eagerly).  Any pointer may be NULL. */
+int ddpg_step_counts(ddpg_ctx* ctx, int64_t* graphed, int64_t* eager, int* capture_failed);
+
 /* ------------------------------------------------------------- profiling */
 /* Enable per-kernel HIP-event timing on the ctx stream (0 disables). */
 int ddpg_profile_enable(ddpg_ctx* ctx, int enable);

@@ -51,7 +51,7 @@ def bench_name(rocprof_name):
     if sym in ("gemm_h_kernel", "gemm_h16_kernel") and len(a) >= 3:
         # bench.py labels it by operand layouts and plane count
         return "%s<%s,%s,NP=%s>" % (sym, a[0], a[1], a[2])
-    if sym == "gemm_h3_kernel" and len(a) == 2:  # three planes by construction
+    if sym in ("gemm_h3_kernel", "gemm_h3m_kernel") and len(a) == 2:  # three planes by construction
         return "%s<%s,%s,NP=3>" % (sym, a[0], a[1])
     if sym == "gemm_h16i_kernel" and len(a) == 2:  # one plane by construction
         return "%s<%s,%s,NP=1>" % (sym, a[0], a[1])

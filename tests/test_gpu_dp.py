@@ -24,7 +24,7 @@ from test_gpu_parity import CONFIGS, GRAD_TOL, _fill, _params, _session, rel
 
 pytestmark = pytest.mark.gpu
 
-ENV = ("DDPG_KCOMB", "DDPG_KCOMB_BLOCKS", "DDPG_GRAPH", "DDPG_GRAPH_COMM", "DDPG_PAR",
+ENV = ("DDPG_KCOMB", "DDPG_KCOMB_BLOCKS", "DDPG_GRAPH", "DDPG_GRAPH_COMM", "DDPG_PAR", "DDPG_GEMM_M16",
        "DDPG_TEST_CS_SPIN", "DDPG_SMALL")
 
 
@@ -86,7 +86,7 @@ def _c3_run(dd, O, p, rows, B, Bg, world=1, proxy=False, profile=False, critic_l
     keys = sorted(prof.read()) if profile else []
     if profile:
         prof.enable(False)
-    out = _state(sess), st, keys
+    out = _state(sess), st, keys, fl.step_counts()
     sess.close()
     return out
 
@@ -101,10 +101,11 @@ def test_small_m_plan_c3_b512(dd, O, clean_env):
     B = 512
     p = _noisy_params(O, S, A, H1, H2, seed=50)
     rows = _rows(np.random.default_rng(9), 6000, S, A, scale)
-    g_state, g_st, _ = _c3_run(dd, O, p, rows, B, B)
-    e_state, e_st, keys = _c3_run(dd, O, p, rows, B, B, profile=True)
-    assert any(k.startswith("gemm_h3_kernel<RK,KR") and k.endswith("/kc") for k in keys), keys
-    assert any(k.startswith("gemm_h3_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
+    g_state, g_st, _, g_cnt = _c3_run(dd, O, p, rows, B, B)
+    e_state, e_st, keys, e_cnt = _c3_run(dd, O, p, rows, B, B, profile=True)
+    assert g_cnt == (1, 0, False) and e_cnt == (0, 1, False), (g_cnt, e_cnt)
+    assert any(k.startswith("gemm_h3m_kernel<RK,KR") and k.endswith("/kc") for k in keys), keys
+    assert any(k.startswith("gemm_h3m_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
     _same(g_state, e_state)
     assert g_st == e_st
     idx = np.array(random.Random(77).sample(range(6000), B))
@@ -128,7 +129,7 @@ def test_kcomb_off_matches_oracle(dd, O, clean_env):
     clean_env.setenv("DDPG_KCOMB", "0")
     p = _noisy_params(O, S, A, H1, H2, seed=51)
     rows = _rows(np.random.default_rng(10), 6000, S, A, scale)
-    state, st, keys = _c3_run(dd, O, p, rows, B, B, profile=True)
+    state, st, keys, _ = _c3_run(dd, O, p, rows, B, B, profile=True)
     assert not any(k.endswith("/kc") for k in keys), keys
     idx = np.array(random.Random(77).sample(range(6000), B))
     L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
@@ -152,10 +153,14 @@ def test_proxy_rank0_of_8_c3(dd, O, clean_env):
     B, Bg, world = 512, 4096, 8
     p = _noisy_params(O, S, A, H1, H2, seed=52)
     rows = _rows(np.random.default_rng(11), 9000, S, A, scale)
-    g_state, g_st, _ = _c3_run(dd, O, p, rows, B, Bg, world=world, proxy=True, critic_lr=0.0)
+    g_state, g_st, _, g_cnt = _c3_run(dd, O, p, rows, B, Bg, world=world, proxy=True,
+                                      critic_lr=0.0)
+    # the RCCL calls were captured with the step (not a silent eager fallback)
+    assert g_cnt == (1, 0, False), g_cnt
     clean_env.setenv("DDPG_GRAPH_COMM", "0")
-    e_state, e_st, keys = _c3_run(dd, O, p, rows, B, Bg, world=world, proxy=True,
-                                  critic_lr=0.0, profile=True)
+    e_state, e_st, keys, e_cnt = _c3_run(dd, O, p, rows, B, Bg, world=world, proxy=True,
+                                         critic_lr=0.0, profile=True)
+    assert e_cnt == (0, 1, False), e_cnt
     assert "rccl_allreduce" in keys and "rccl_stats" in keys, keys
     assert any(k.startswith("xwin|") for k in keys), keys
     _same(g_state, e_state)
@@ -181,8 +186,9 @@ def _wide_comm(dd, O, name, p, spin=0, comm=True):
         init_comm(sess, 0, 1, single=True)
     rb = ReplayBuffer(5000, 1234)
     _fill(rb, S, A, 3000, scale, seed=2)
-    st = FusedLearner(sess, rb, 1024).step(stats=True)
-    out = _state(sess), st
+    fl = FusedLearner(sess, rb, 1024)
+    st = fl.step(stats=True)
+    out = _state(sess), st, fl.step_counts()
     sess.close()
     return out
 
@@ -196,6 +202,9 @@ def test_comm_graph_matches_no_comm(dd, O, clean_env, graph_comm):
     ref = _wide_comm(dd, O, "wide", p, comm=False)
     clean_env.setenv("DDPG_GRAPH_COMM", graph_comm)
     got = _wide_comm(dd, O, "wide", p)
+    # graph_comm=1: the step was replayed from a graph holding the RCCL calls
+    # (a failed capture would fall back to eager and pass the equality trivially)
+    assert got[2] == ((1, 0, False) if graph_comm == "1" else (0, 1, False)), got[2]
     _same(got[0], ref[0])
     assert got[1] == ref[1]
 
@@ -217,6 +226,7 @@ def test_comm_stream_ordering_spin(dd, O, clean_env, par, graph_comm):
     ref = _wide_comm(dd, O, "wide", p)
     clean_env.setenv("DDPG_TEST_CS_SPIN", "300")
     got = _wide_comm(dd, O, "wide", p)
+    assert got[2] == ((1, 0, False) if graph_comm == "1" else (0, 1, False)), got[2]
     state, ref_state = got[0], ref[0]
     for g, g0 in zip(state[9], ref_state[9]):           # critic gradient
         assert np.array_equal(g, 2 * g0)

@@ -19,7 +19,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       gemm_h16_kernel) instead of gemm_h3_kernel / gemm_h16i_kernel
                       (gemm_h3.h): same products, same order (fp32 and bf16;
                       both on the unsplit plan, DDPG_KCOMB=0, since only the
-                      gemm_h3.h kernels combine in-launch K splits)
+                      gemm_h3.h kernels combine in-launch K splits; fp32 with
+                      DDPG_GEMM_M16=0 on both sides, the 32x32x16 forms)
     DDPG_TK_RPB=3     thin_k blocks walk 3 row tiles each (W panel staged once,
                       next X tile prefetched) instead of the automatic count
     DDPG_GEMM_PACK=0  the bf16 configuration's S > 64 first layers launched one
@@ -37,6 +38,9 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_THINK=0      the K <= 64 layers on the tiled GEMMs instead of thin_k
     DDPG_SKINNY=0     the <= 64-wide weight gradients on the GEMMs instead of
                       the skinny VALU kernel
+    DDPG_GEMM_M16=0   the fp32 forward / dX twin GEMMs on gemm_h3_kernel
+                      (32x32x16 MFMA) instead of gemm_h3m_kernel (16x16x32:
+                      32 products per MFMA instead of 16, fp32 rounding differs)
   bf16 configuration, different summation order -- the oracle's bf16 bars,
   and the two paths' gradients against each other:
     DDPG_GEMM256=1    the split-K weight gradients on the 256 x 256-tile GEMM
@@ -57,7 +61,8 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_M
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
-            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL")
+            "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
+            "DDPG_GEMM_M16")
 
 
 @pytest.fixture(scope="module")
@@ -152,8 +157,10 @@ def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
     if switch == "DDPG_GEMM_H3":
         # gemm_h_kernel has no in-launch K split (small-M plan): compare both
-        # kernels on the same unsplit plan
+        # kernels on the same unsplit plan; and the 32x32x16 forms on both
+        # sides (gemm_h3_kernel vs gemm_h_kernel: same products, same order)
         monkeypatch.setenv("DDPG_KCOMB", "0")
+        monkeypatch.setenv("DDPG_GEMM_M16", "0")
     p, _ = _params(O, name)
     ref = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
     monkeypatch.setenv(switch, value)
@@ -279,7 +286,8 @@ def test_gemm256_switch_bf16(dd, O, monkeypatch):
 @pytest.mark.parametrize("switch,value,kernel,absent", [
     ("DDPG_GEMM", "f32", "gemm_f32_kernel", "gemm_h"),
     ("DDPG_GEMM_H", "0", "gemm_s3_kernel", "gemm_h"),
-    ("DDPG_THINK", "0", "gemm_h3_kernel", "thin_k_kernel"),
+    ("DDPG_THINK", "0", "gemm_h3m_kernel", "thin_k_kernel"),
+    ("DDPG_GEMM_M16", "0", "gemm_h3_kernel<RK,KR", "gemm_h3m_kernel"),
     ("DDPG_SKINNY", "0", "gemm_f32_kernel", "skinny_wgrad_kernel"),
 ])
 def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent):
