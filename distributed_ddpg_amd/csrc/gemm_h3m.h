@@ -167,12 +167,18 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
   bf16x8 fa[2][NP][TA], fb[2][NP][TB];
   constexpr int NRG = NP * (TA + TB);  // 18 read groups per k-tile
   constexpr int NMF = TA * TB * 6;     // 48 MFMAs per k-tile
-  constexpr int DG0 = NRG + 2, DGS = 4;  // LDS-DMA pieces in gaps DG0, DG0 + DGS, ...
+#ifndef H3M_DG0  // schedule knobs (tools/h3_phase_bench.hip sweeps them)
+#define H3M_DG0 (NRG + 2)
+#define H3M_DGS 4
+#define H3M_RPG 1
+#endif
+  constexpr int DG0 = H3M_DG0, DGS = H3M_DGS;  // LDS-DMA pieces in gaps DG0, DG0 + DGS, ...
+  constexpr int RPG = H3M_RPG;                  // read groups per MFMA gap
   static_assert(DG0 + DGS * (C::G - 1) < NMF, "DMA gaps");
   // k-tile t in slot SL with fragment set PAR.  st: stage tile t+3 into slot
   // SL after X_t; nx: tile t+1 exists (read in this tile's gaps); g2: tile
   // t+2 is in flight (vmcnt(G) at X_t leaves it there)
-  auto tile = [&](int t, auto sl_c, auto par_c, bool st, bool nx, bool g2) {
+  auto tile = [&](int t, auto sl_c, auto par_c, bool st, bool nx, bool g2) __attribute__((always_inline)) {
     constexpr int SL = decltype(sl_c)::value;
     constexpr int PAR = decltype(par_c)::value;
     auto& av = fa[PAR];
@@ -192,11 +198,14 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
     static_for<NMF>([&](auto q_c) {
       constexpr int q = decltype(q_c)::value;
       mfma_q(q_c, av, bv);
-      if constexpr (q < NRG) {
-        if (nx)
-          read_one(std::integral_constant<int, (SL + 1) % 3>{}, std::integral_constant<int, q>{},
-                   nav, nbv);
-      }
+      static_for<RPG>([&](auto r_c) {
+        constexpr int J = RPG * q + decltype(r_c)::value;
+        if constexpr (J < NRG) {
+          if (nx)
+            read_one(std::integral_constant<int, (SL + 1) % 3>{}, std::integral_constant<int, J>{},
+                     nav, nbv);
+        }
+      });
       if constexpr (q >= DG0 && (q - DG0) % DGS == 0 && (q - DG0) / DGS < C::G) {
         if (st) piece(t + 3, sl_c, (q - DG0) / DGS);
       }
@@ -228,6 +237,9 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
     __builtin_amdgcn_sched_barrier(0);
 #ifdef DDPG_H3_STAMP_PROLOGUE
     KC_STAMP(2)
+#endif
+#if defined(H3M_PRIO) && H3M_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // schedule knob (bench only)
 #endif
     int t = 0;
     // full trips of six tiles (slots 0 1 2 0 1 2, sets 0 1 0 1 0 1), every
