@@ -209,6 +209,7 @@ def per_rank_step(cfg_name, device, n, mode, rb, dtype, steps=30, warmup=5, prof
     sess, _, fl, _ = build_learner(cfg_name, device, 0, n, 0, dtype=dtype, per_gpu_b=b, rb=rb,
                                    proxy=True)
     el = timed(fl, sess, steps, warmup, 1)
+    graphed, eager, failed = fl.step_counts()   # the timed steps: graph replays?
     rows, _ = kernel_profile(fl, sess, prof_steps)
     sess.close()
     win = {k.split("|", 1)[1]: 1e3 * v["ms"] / v["launches"] for k, v in rows.items()
@@ -218,6 +219,8 @@ def per_rank_step(cfg_name, device, n, mode, rb, dtype, steps=30, warmup=5, prof
     top = sorted(((k, v) for k, v in by_kernel.items() if not k.startswith("xwin")),
                  key=lambda kv: -kv[1]["ms"])[:8]
     return {"per_rank_batch": b, "step_ms": round(1000.0 * el / steps, 4),
+            "step_mode": {"graph_replays": graphed, "eager_steps": eager,
+                          "rccl_capture_failed": failed},
             "gpu_busy_ms": round(busy, 4),
             "window_us": {k: round(v, 1) for k, v in win.items()},
             "kernels_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in top}}
@@ -230,7 +233,9 @@ def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
     measured 1-GPU updates/s (no communicator)."""
     S, A, H1, H2 = CONFIGS[cfg_name][:4]
     xb = exchange_bytes(S, A, H1, H2)
-    out = {"model": {"xgmi_link_GBs_per_direction": XGMI_LINK_GBS, "rccl_bus_efficiency": RCCL_EFF,
+    out = {"value_kind": "projected: measured per-rank step + modelled exchange "
+                         "(model inputs below are assumptions; N >= 2 unmeasured on hardware)",
+           "model": {"xgmi_link_GBs_per_direction": XGMI_LINK_GBS, "rccl_bus_efficiency": RCCL_EFF,
                      "rccl_latency_us": RCCL_LAT_US, "exchange_bytes": xb,
                      "formula": "step(N) = measured per-rank step (proxy communicator, graph) "
                                 "+ sum over the 4 calls of max(0, T_ar(bytes, N) - overlap "
@@ -556,6 +561,7 @@ def main():
         print(json.dumps({"metric": "projected actor+critic updates/sec on %d GPUs (%s scaling, "
                                     "rank 0's workload measured on one GPU)" % (n, args.scaling),
                           "value": pr[args.scaling][str(n)]["projected_updates_s"],
+                          "value_kind": "projected", "measured_on_n_gpus": 1,
                           "unit": "updates/s", "n_gpus": 1, "per_rank_of": n,
                           "scaling": args.scaling, "dtype": dtype, "config": {"workload": label},
                           "projected_scaling": pr}), flush=True)

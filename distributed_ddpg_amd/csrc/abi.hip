@@ -41,8 +41,7 @@ static void ctx_free(ddpg_ctx* c) {
     if (g.done) (void)hipEventDestroy(g.done);
   }
   if (c->step_done) (void)hipEventDestroy(c->step_done);
-  for (void* p : {(void*)c->sb_save, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T,
-                  (void*)c->sb_stamps})
+  for (void* p : {(void*)c->sb_save, (void*)c->sb_misc, (void*)c->sb_whT, (void*)c->sb_w2T})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->atw, (void*)c->wtw, (void*)c->kc_part, (void*)c->kc_ticket})
     if (p) (void)hipFree(p);
@@ -154,7 +153,6 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_h = !env_is("DDPG_GEMM_H", "0");
       c->sw.gemm_s3 = !env_is("DDPG_GEMM", "f32");
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
-      c->sw.gemm_mf = env_is("DDPG_GEMM_MF", "32") ? 32 : 16;
       c->sw.gemm_h3 = !env_is("DDPG_GEMM_H3", "0");
       c->sw.gemm_m16 = !env_is("DDPG_GEMM_M16", "0");
       if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = atoi(v) == 1;
@@ -280,19 +278,6 @@ void ddpg_destroy(ddpg_ctx* c) {
 int ddpg_sync(ddpg_ctx* c) {
   return guard(c, [&] {
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->sb_stamps) {  // diagnostic: per-op cycle counts of the last small-batch step
-      unsigned long long t[64];
-      HIP_TRY(hipMemcpy(t, c->sb_stamps, sizeof t, hipMemcpyDeviceToHost));
-      fprintf(stderr, "[sb stamps] phase1:");
-      for (int i = 1; i <= 10; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
-      fprintf(stderr, " total %llu | phase3:", t[10] - t[0]);
-      for (int i = 33; i <= 42; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
-      fprintf(stderr, " total %llu | wgrad c:", t[42] - t[32]);
-      for (int i = 49; i <= 50; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
-      fprintf(stderr, " | wgrad a:");
-      for (int i = 57; i <= 58; ++i) fprintf(stderr, " %llu", t[i] - t[i - 1]);
-      fprintf(stderr, "\n");
-    }
   });
 }
 

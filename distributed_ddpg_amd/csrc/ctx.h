@@ -252,7 +252,6 @@ struct ddpg_ctx {
   int td_nqt = 0;      // fused step: target-critic partials pending in qpart_t for critic_loss
   int sb_xstride = 0;  // XCD packing of the phase kernels: 0 auto (on up to 32 workgroups),
                        // env DDPG_SB_XCD=1 always (8), =0 never (1)
-  unsigned long long* sb_stamps = nullptr;  // diagnostic (env DDPG_SB_STAMPS=1)
 
   // kernel-path switches, read from the environment at ddpg_create (each is
   // exercised by tests/test_gpu_switches.py)
@@ -260,7 +259,6 @@ struct ddpg_ctx {
     bool gemm_h = true;    // DDPG_GEMM_H=0: no bf16-twin GEMM (gemm_s3 NP=3 instead)
     bool gemm_s3 = true;   // DDPG_GEMM=f32: the fp32-input MFMA kernel for every GEMM
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
-    int gemm_mf = 16;      // DDPG_GEMM_MF=32: bf16 config on the 32x32x16 twin GEMM
     bool gemm_h3 = true;   // DDPG_GEMM_H3=0: twin GEMMs with runtime slot addressing (gemm_h_kernel / gemm_h16_kernel)
     bool gemm_m16 = true;  // DDPG_GEMM_M16=0: fp32 contexts on the 32x32x16 gemm_h3_kernel instead of gemm_h3m_kernel
     int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h (opt-in)

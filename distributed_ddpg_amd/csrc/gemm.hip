@@ -186,7 +186,7 @@ static int h256_splits(int M, int N, int K, int cap) {
 // default: in the C5 step the finer split's extra slab reduction cost more
 // than the faster main loop saved (profiles/r3/gemm_h256_ab_c5.txt).
 static int h256_mode(const ddpg_ctx* c, int M, int N, int Kh, int splits, const GemmEpi& e) {
-  if (!(c->hnp == 1 && c->sw.gemm256 && c->sw.gemm_mf == 16 && M % H2_BM == 0 &&
+  if (!(c->hnp == 1 && c->sw.gemm256 && M % H2_BM == 0 &&
         N % H2_BN == 0 && Kh % 128 == 0))
     return -1;
   const bool plain = !e.bias && e.act == 0 && e.post == 0 && !e.colsum && !e.proj_out && !e.outh;
@@ -257,8 +257,7 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       // has 32 forward tiles for 256 CUs -- splits K over ~256 blocks (>= 3
       // k-tiles each) and combines the splits in-launch before its epilogue
       // (ksplit_combine).  The immediate-offset kernels only.
-      const bool kc_kernel = c->sw.gemm_h3 && (c->hnp == 3 || (c->hnp == 1 && c->sw.gemm_mf == 16 &&
-                                                              AL == L_RK));
+      const bool kc_kernel = c->sw.gemm_h3 && (c->hnp == 3 || (c->hnp == 1 && AL == L_RK));
       if (splits_req == 1 && kc_kernel && c->kc_part) {
         const int tiles = h.nt(N) * h.mt(M);
         const int nkt = Kh / BKh;
@@ -318,8 +317,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
         HIP_TRY(hipGetLastError());
         return q;
       }
-      // bf16 configuration: the 16x16x32-MFMA kernel (DDPG_GEMM_MF=32 keeps 32x32x16)
-      const bool h16 = c->hnp == 1 && c->sw.gemm_mf == 16;
+      // bf16 configuration: the 16x16x32-MFMA kernels
+      const bool h16 = c->hnp == 1;
       // fp32 contexts: RK-A GEMMs (forward, dX) on the 16x16x32 form
       const bool m16 = c->hnp == 3 && AL == L_RK && c->sw.gemm_m16;
       char key[112];
@@ -355,8 +354,6 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
           hipLaunchKernelGGL((gemm_h16i_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
       } else if (h16)
         hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
-      else if (c->hnp == 1)
-        hipLaunchKernelGGL((gemm_h_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else if (c->sw.gemm_h3 && m16) {
         // the same six plane products on the 16x16x32 MFMA (gemm_h3m.h), RK A operands
         if constexpr (AL == L_RK)

@@ -93,7 +93,9 @@ struct SbArgs {
   double* acc;           // [qmax_sum, loss_sum, steps]
   long long aW1, ab1, aW2, ab2, aW3;
   long long cWs, cbs, cWa, cba, cWh, cbh, cWo, cbo;
-  unsigned long long* stamps;  // diagnostic (env DDPG_SB_STAMPS): WG 0 s_memtime per level
+#ifdef DDPG_SB_STAMPS
+  unsigned long long* stamps;  // diagnostic build only: WG 0 s_memtime per level
+#endif
   // XCD packing: the grid has xstride x G blocks and only every xstride-th
   // works, so with the hardware's round-robin block->XCD dealing all working
   // WGs share one XCD's L2 and the weights stream from it once rather than
@@ -101,12 +103,29 @@ struct SbArgs {
   int xstride;
 };
 
-// Diagnostic stamp: nothing reads it on device and no output depends on it.
+// Diagnostic stamps (a -DDDPG_SB_STAMPS build only; the product compiles
+// them away): nothing reads them on device and no output depends on them.
+#ifdef DDPG_SB_STAMPS
 #define SB_STAMP(i)                                                              \
   do {                                                                           \
     if (g.stamps && blockIdx.x == 0 && threadIdx.x == 0)                         \
       g.stamps[i] = __builtin_amdgcn_s_memtime();                                \
   } while (0)
+#define SB_STAMP_SYNC(i)                                                         \
+  do {                                                                           \
+    if (g.stamps) {                                                              \
+      __syncthreads();                                                           \
+      SB_STAMP(i);                                                               \
+    }                                                                            \
+  } while (0)
+#else
+#define SB_STAMP(i) \
+  do {              \
+  } while (0)
+#define SB_STAMP_SYNC(i) \
+  do {                   \
+  } while (0)
+#endif
 
 // LDS floats a phase workgroup needs (host side: launch size and eligibility).
 inline size_t sb_smem_floats(int LX, int LW) {
@@ -499,10 +518,7 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   sb_save(g.sv.dcat, g.sv.Bp, 2 * g.CH1, b3, r0);
   sb_save(g.sv.h, g.sv.Bp, g.CH2, h, r0);
   sb_save(g.sv.dhp, g.sv.Bp, g.CH2, b2, r0);
-  if (g.stamps) {
-    __syncthreads();
-    SB_STAMP(10);
-  }
+  SB_STAMP_SYNC(10);
 }
 
 __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
@@ -585,10 +601,7 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   sb_save(g.sv.dz1, g.sv.Bp, g.AH1, cat, r0);
   sb_save(g.sv.dz2, g.sv.Bp, g.AH2, dh, r0);
   sb_save(g.sv.dz3, g.sv.Bp, g.A, dz3, r0);
-  if (g.stamps) {
-    __syncthreads();
-    SB_STAMP(42);
-  }
+  SB_STAMP_SYNC(42);
 }
 
 // Action selection (ddpg.py:68-70, actor.predict at B = 1 .. 64): the whole
@@ -644,7 +657,9 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
 constexpr int SB_GU = 16;  // float4s (4 batch rows each) per batch of loads
 __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTab tab, int net,
                                                               int nslab) {
+#ifdef DDPG_SB_STAMPS
   const int sbase = net == 1 ? 48 : 56;
+#endif
   SB_STAMP(sbase);
   int ti = 0;
 #pragma unroll

@@ -637,7 +637,7 @@ static bool first_layers_dev(ddpg_ctx* c, int B) {
   if (thin_k_launch(c, "fwd_l1", tp, TK_MAXP, B)) return true;
   // S > 64 (the bf16 configuration C5: S = 376): each part on thin_k where
   // it takes it, the rest as ONE gemm_h16i_pack_kernel launch (gemm_flush)
-  if (!(c->hnp == 1 && c->sw.gemm_h3 && c->sw.gemm_mf == 16)) return false;
+  if (!(c->hnp == 1 && c->sw.gemm_h3)) return false;
   c->gemm_defer = 1;
   for (int i = 0; i < TK_MAXP; ++i) {
     if (thin_k_launch(c, "fwd_l1", &tp[i], 1, B)) continue;
@@ -774,7 +774,6 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   a.cbh = L.c[CBH].off;
   a.cWo = L.c[CWO].off;
   a.cbo = L.c[CBO].off;
-  a.stamps = c->sb_stamps;
   // all workgroups on one XCD (one L2 streams the weights) while they fit its
   // 32 CUs: +3 % at C2 (profiles/r3/sb_xcd_ab_c2.txt)
   a.xstride = c->sb_xstride ? c->sb_xstride : (ceil_div(B, SB_R) <= 32 ? 8 : 1);
@@ -962,11 +961,6 @@ void sb_setup(ddpg_ctx* c) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     HIP_TRY(hipHostMalloc(&c->h_pred, (size_t)c->Bmax * c->A * sizeof(float)));
     c->sb_ok = true;
-    if (const char* st = getenv("DDPG_SB_STAMPS"))
-      if (atoi(st)) {
-        HIP_TRY(hipMalloc(&c->sb_stamps, 64 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(c->sb_stamps, 0, 64 * sizeof(unsigned long long)));
-      }
   }
 }
 

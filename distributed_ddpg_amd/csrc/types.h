@@ -12,8 +12,9 @@ namespace ddpg {
 enum { L_RK = 0, L_KR = 1 };
 
 // in-launch K split (ksplit_combine, gemm_common.h): at most KC_MAXS splits
-// per tile (the host's default cap is 4, DDPG_KCOMB_SPLITS up to KC_MAXS)
-constexpr int KC_MAXS = 8;
+// per tile (DDPG_KCOMB_SPLITS=2 / 3 lowers the cap; 8 splits measured slower
+// at the per-rank B = 512 shapes, profiles/r4/per_rank_split8.txt)
+constexpr int KC_MAXS = 4;
 constexpr int GBK = 32, GNT = 256;
 constexpr int PROJ_MAX = 32;
 

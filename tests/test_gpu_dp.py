@@ -241,3 +241,39 @@ def test_comm_stream_ordering_spin(dd, O, clean_env, par, graph_comm):
             g = g.astype(np.float32)
             assert np.array_equal(m, (g - np.float32(0)) * c1)
             assert np.array_equal(v, (g * g - np.float32(0)) * c2)
+
+
+def test_ksplit_combine_deterministic_c5_b1024(dd, O, clean_env):
+    """The in-launch K split at a second shape: the bf16 configuration at C5
+    widths (S = 376, A = 17, 2048 / 2048) with B = 1024 (rank 0 of a 4-rank
+    strong run), where the forward and dX gemm_h16i launches split K and
+    combine in-launch.  Two fresh sessions run the same three fused steps --
+    every gradient, Adam slot and parameter is bitwise equal between them
+    (the combine adds the splits in split order, whatever order they land
+    in), and the split launches really ran ("/kc" keys)."""
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale = 376, 17, 2048, 2048, 1.0
+    B = 1024
+    p = _noisy_params(O, S, A, H1, H2, seed=53)
+    rows = _rows(np.random.default_rng(12), 3000, S, A, scale)
+    runs = []
+    for rep in range(2):
+        sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B, dtype="bf16")
+        rb = ReplayBuffer(4000, 99)
+        rb.add_batch(*rows)
+        fl = FusedLearner(sess, rb, B)
+        prof = Profile(sess)
+        if rep == 1:
+            prof.enable(True)
+        st = [fl.step(stats=True) for _ in range(3)]
+        keys = sorted(prof.read()) if rep == 1 else []
+        if rep == 1:
+            prof.enable(False)
+        runs.append((_state(sess), st, keys))
+        sess.close()
+    keys = runs[1][2]
+    assert any(k.startswith("gemm_h16i_kernel<RK,KR") and k.endswith("/kc") for k in keys), keys
+    assert any(k.startswith("gemm_h16i_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
+    assert runs[0][1] == runs[1][1]
+    _same(runs[0][0], runs[1][0])

@@ -9,8 +9,6 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_PAR=1        independent branches forked onto two aux streams
     DDPG_SB_XCD=0     small-batch workgroups dealt over the XCDs (the default
                       packs up to 32 of them on one XCD)
-    DDPG_GEMM_MF=32   bf16 config on the 32x32x16 twin GEMM (same per-output
-                      summation order as the default 16x16x32 kernel)
     DDPG_L1BATCH=0    the large-batch step's first layers launched per network
                       instead of as one five-part thin_k launch
     DDPG_ACT32=1      fp32 copies of h1 / cat / cat2 written beside their planes
@@ -56,7 +54,7 @@ from test_gpu_parity import (CONFIGS, GRAD_TOL, FWD_TOL, _fill, _params, _sessio
 
 pytestmark = pytest.mark.gpu
 
-SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM_MF", "DDPG_GEMM",
+SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_GEMM_H", "DDPG_THINK", "DDPG_GRAPH", "DDPG_SMALL", "DDPG_SKINNY", "DDPG_L1BATCH",
             "DDPG_ACT32", "DDPG_GEMM256", "DDPG_GEMM_H3", "DDPG_TK_RPB",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
@@ -170,22 +168,6 @@ def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
             assert any(k.startswith("thin_k_kernel" + form) for k in ref["keys"]), ref["keys"]
         assert not any(k.startswith(("thin_k_kernel<FWD>", "thin_k_kernel<BWD>"))
                        for k in got["keys"]), got["keys"]
-    _bitwise(got, ref)
-
-
-def test_gemm_mf32_bf16_bitwise(dd, O, monkeypatch):
-    """bf16 configuration: the 32x32x16 twin GEMM (DDPG_GEMM_MF=32) against the
-    default 16x16x32 kernel -- bitwise -- and against the oracle at the stated
-    bf16 bar."""
-    _clear(monkeypatch)
-    monkeypatch.setenv("DDPG_KCOMB", "0")  # gemm_h_kernel has no in-launch K split
-    p, _ = _params(O, "wide")
-    ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
-    assert any(k.startswith("gemm_h16") for k in ref["keys"]), ref["keys"]
-    monkeypatch.setenv("DDPG_GEMM_MF", "32")
-    got = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
-    assert any(k.startswith("gemm_h_kernel") and "NP=1" in k for k in got["keys"]), got["keys"]
-    assert not any(k.startswith("gemm_h16_kernel") for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 
