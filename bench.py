@@ -46,13 +46,16 @@ CONFIGS = {
            "C3 synthetic S=64 A=16 actor/critic 1024/1024, batch 4096/GPU"),
     "c2": (4, 1, 128, 200, 64, 3.0,
            "C2 InvertedPendulum-shaped S=4 A=1 128/200, batch 64"),
+    # the reference's own default batch (parameters.py:11)
+    "c2b": (4, 1, 128, 200, 256, 3.0,
+            "C2 InvertedPendulum-shaped S=4 A=1 128/200, batch 256 (parameters.py:11)"),
     "c5": (376, 17, 2048, 2048, 4096, 1.0,
            "C5 Humanoid-shaped S=376 A=17 2048/2048, batch 4096/GPU"),
     # BASELINE configs[0]: MountainCar-shaped, 400/300 MLP, batch 64 (CPU leg)
     "c1": (2, 1, 400, 300, 64, 1.0,
            "C1 MountainCar-shaped S=2 A=1 400/300, batch 64"),
 }
-DEFAULT_DTYPE = {"c3": "fp32", "c2": "fp32", "c5": "bf16", "c1": "fp32"}
+DEFAULT_DTYPE = {"c3": "fp32", "c2": "fp32", "c2b": "fp32", "c5": "bf16", "c1": "fp32"}
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # ~2.5 PF dense (MI355X_MICROARCH.md)
 # fp32 GEMMs on the bf16 pipe (gemm_s3): six bf16 MFMA products per fp32 MAC,
 # so the pipe bounds fp32-equivalent throughput at 2.5 PF / 6
@@ -178,20 +181,25 @@ def allreduce_us(nbytes, n, eff=RCCL_EFF):
     return RCCL_LAT_US[n] + 2.0 * (n - 1) / n * nbytes / (busbw * 1e3)
 
 
-def exchange_bytes(S, A, H1, H2):
+def exchange_bytes(S, A, H1, H2, elt=4):
     """Bytes of each RCCL call of one data-parallel step (the ctx's flat
     layout: critic dWh, the critic's other tensors + stats, actor dW2, the
-    actor's other tensors), fp32."""
+    actor's other tensors): fp32 (elt 4), or bf16 (elt 2) in the bf16
+    configuration, whose exchange payload is bf16."""
     ap = S * H1 + H1 + H1 * H2 + H2 + H2 * A
     cp = S * H1 + H1 + A * H1 + H1 + 2 * H1 * H2 + H2 + H2 + 1
-    return {"critic_dWh": 4 * 2 * H1 * H2, "critic_rest": 4 * (cp - 2 * H1 * H2) + 8,
-            "actor_dW2": 4 * H1 * H2, "actor_rest": 4 * (ap - H1 * H2)}
+    return {"critic_dWh": elt * 2 * H1 * H2, "critic_rest": elt * (cp - 2 * H1 * H2) + 8,
+            "actor_dW2": elt * H1 * H2, "actor_rest": elt * (ap - H1 * H2)}
 
 
-def exposed_exchange_us(xb, win_c_us, win_a_us, n, eff=RCCL_EFF):
+def exposed_exchange_us(xb, win_c_us, win_a_us, n, eff=RCCL_EFF, small=False):
     """Exchange time on the critical path of one step: the dWh / dW2
     all-reduces overlap the measured windows (the compute issued between the
-    exchange and the join), the tail calls are fully exposed."""
+    exchange and the join), the tail calls are fully exposed.  small: the
+    small-batch path's two calls (one per network, nothing to overlap)."""
+    if small:
+        return (allreduce_us(xb["critic_dWh"] + xb["critic_rest"], n, eff) +
+                allreduce_us(xb["actor_dW2"] + xb["actor_rest"], n, eff))
     t = max(0.0, allreduce_us(xb["critic_dWh"], n, eff) - win_c_us)
     t += allreduce_us(xb["critic_rest"], n, eff)
     t += max(0.0, allreduce_us(xb["actor_dW2"], n, eff) - win_a_us)
@@ -221,6 +229,8 @@ def per_rank_step(cfg_name, device, n, mode, rb, dtype, steps=30, warmup=5, prof
     return {"per_rank_batch": b, "step_ms": round(1000.0 * el / steps, 4),
             "step_mode": {"graph_replays": graphed, "eager_steps": eager,
                           "rccl_capture_failed": failed},
+            "path": "small-batch kernels" if any(k.startswith("sb_") for k in rows)
+                    else "large-batch GEMM path",
             "gpu_busy_ms": round(busy, 4),
             "window_us": {k: round(v, 1) for k, v in win.items()},
             "kernels_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in top}}
@@ -232,14 +242,15 @@ def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
     exchange exposed beyond the measured overlap windows.  base_value = the
     measured 1-GPU updates/s (no communicator)."""
     S, A, H1, H2 = CONFIGS[cfg_name][:4]
-    xb = exchange_bytes(S, A, H1, H2)
+    xb = exchange_bytes(S, A, H1, H2, 2 if dtype == "bf16" else 4)
     out = {"value_kind": "projected: measured per-rank step + modelled exchange "
                          "(model inputs below are assumptions; N >= 2 unmeasured on hardware)",
            "model": {"xgmi_link_GBs_per_direction": XGMI_LINK_GBS, "rccl_bus_efficiency": RCCL_EFF,
                      "rccl_latency_us": RCCL_LAT_US, "exchange_bytes": xb,
                      "formula": "step(N) = measured per-rank step (proxy communicator, graph) "
                                 "+ sum over the 4 calls of max(0, T_ar(bytes, N) - overlap "
-                                "window); T_ar = lat + 2(N-1)/N bytes / ((N-1) link eff); "
+                                "window) (small-batch path: its 2 calls, fully exposed); "
+                                "T_ar = lat + 2(N-1)/N bytes / ((N-1) link eff); "
                                 "pessimistic: eff halved"},
            "measured_1gpu_updates_s": base_value}
     for mode in ("strong", "weak"):
@@ -248,8 +259,9 @@ def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
             m = per_rank_step(cfg_name, device, n, mode, rb, dtype)
             wc = m["window_us"].get("critic", 0.0)
             wa = m["window_us"].get("actor", 0.0)
-            ex = exposed_exchange_us(xb, wc, wa, n)
-            ex_p = exposed_exchange_us(xb, wc, wa, n, RCCL_EFF / 2)
+            small = m["path"] == "small-batch kernels"
+            ex = exposed_exchange_us(xb, wc, wa, n, small=small)
+            ex_p = exposed_exchange_us(xb, wc, wa, n, RCCL_EFF / 2, small=small)
             step = m["step_ms"] + ex / 1000.0
             step_p = m["step_ms"] + ex_p / 1000.0
             # strong: global updates/s; weak: batch-B updates processed by all ranks / s
@@ -674,6 +686,26 @@ def main():
             "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1),
             "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
         s2.close()
+        # the reference's default batch (B = 256): one GPU, and rank 0 of an
+        # 8-rank data-parallel run at that per-rank batch (weak: the
+        # reference's workers each train on their own 256 rows)
+        s2b, _, fl2b, _ = build_learner("c2b", local, 0, 1, 0, rb=rb2)
+        el2b = timed(fl2b, s2b, 300, 30, 1)
+        lat2b = step_latency_percentiles(fl2b, s2b, 200)
+        rows2b, _ = kernel_profile(fl2b, s2b, 50)
+        s2b.close()
+        dp2b = per_rank_step("c2b", local, 8, "weak", rb2, "fp32")
+        out["small_batch"]["b256"] = {
+            "workload": CONFIGS["c2b"][6], "value": round(300 / el2b, 1), "unit": "updates/s",
+            "ms_per_step": round(1000 * el2b / 300, 4), "step_latency": lat2b,
+            "path": "small-batch kernels" if any(k.startswith("sb_") for k in rows2b)
+                    else "large-batch GEMM path",
+            "kernels_per_step": sum(r["launches"] for r in rows2b.values()) / 50,
+            "gpu_busy_ms_per_step": round(sum(r["ms"] for r in rows2b.values()) / 50, 4),
+            "dp_rank0_of_8_weak": dict(dp2b, note="rank 0's step of an 8-rank data-parallel "
+                                       "run at 256 rows per rank, measured through the 1-rank "
+                                       "proxy communicator (RCCL calls as identities: the "
+                                       "8-rank exchange itself is not included)")}
     if not args.no_small and cfg == "c3":
         # BASELINE configs[4] (C5, bf16) as a secondary line on every rank: same
         # step, same accounting and scaling mode, its own dominant kernel

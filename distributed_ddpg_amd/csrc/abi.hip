@@ -46,7 +46,8 @@ static void ctx_free(ddpg_ctx* c) {
   for (void* p : {(void*)c->atw, (void*)c->wtw, (void*)c->kc_part, (void*)c->kc_ticket})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
-                  (void*)c->dmean, (void*)c->dscale, (void*)c->dacc, (void*)c->dstats_all})
+                  (void*)c->dmean, (void*)c->dscale, (void*)c->dacc, (void*)c->dstats_all,
+                  (void*)c->xbuf})
     if (p) (void)hipFree(p);
   for (auto st : c->aux)
     if (st) (void)hipStreamDestroy(st);

@@ -178,6 +178,7 @@ struct ddpg_ctx {
   unsigned* dcounter = nullptr;  // [2]
   float* dstats = nullptr;       // [q_max, loss]
   float* dstats_all = nullptr;   // [world][2] all-gathered stats (world > 1)
+  __bf16* xbuf = nullptr;        // bf16 configuration: the exchange's bf16 payload (L.total)
   double* dacc = nullptr;        // [qmax_sum, loss_sum, steps]
   double *dmean = nullptr, *dscale = nullptr;
   bool has_scaler = false;

@@ -37,6 +37,37 @@ __global__ void cs_spin_scale_kernel(float* b0, long long n0, float* b1, long lo
   for (long long i = i0; i < n1; i += stride) b1[i] = 2.f * b1[i];
 }
 
+// bf16 configuration's exchange payload: the rank's fp32 gradient rounded
+// to bf16 (one rounding, as the bf16 GEMM operands), summed by RCCL in bf16,
+// widened back into the fp32 gradient buffer for Adam
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, long long n,
+                                   __bf16* __restrict__ y) {
+  const long long i0 = 4 * ((long long)blockIdx.x * blockDim.x + threadIdx.x);
+  const long long stride = 4ll * gridDim.x * blockDim.x;
+  for (long long i = i0; i < n; i += stride) {
+    if (i + 4 <= n) {
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      y[i] = (__bf16)v.x;
+      y[i + 1] = (__bf16)v.y;
+      y[i + 2] = (__bf16)v.z;
+      y[i + 3] = (__bf16)v.w;
+    } else {
+      for (long long j = i; j < n; ++j) y[j] = (__bf16)x[j];
+    }
+  }
+}
+__global__ void bf16_to_f32_kernel(const __bf16* __restrict__ y, long long n,
+                                   float* __restrict__ x) {
+  const long long i0 = 4 * ((long long)blockIdx.x * blockDim.x + threadIdx.x);
+  const long long stride = 4ll * gridDim.x * blockDim.x;
+  for (long long i = i0; i < n; i += stride) {
+    if (i + 4 <= n)
+      *reinterpret_cast<float4*>(x + i) =
+          make_float4((float)y[i], (float)y[i + 1], (float)y[i + 2], (float)y[i + 3]);
+    else
+      for (long long j = i; j < n; ++j) x[j] = (float)y[j];
+  }
+}
 
 static void nccl_try(ncclResult_t r) {
   if (r != ncclSuccess) throw DdpgError(DDPG_ECOMM, ncclGetErrorString(r));
@@ -78,20 +109,45 @@ void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0
                        b1, (long long)n1, c->test_cs_spin);
     HIP_TRY(hipGetLastError());
   }
+  // bf16 configuration: half the bytes on the links
+  const bool half = c->xbuf != nullptr;
+  __bf16* h0 = half ? c->xbuf : nullptr;
+  __bf16* h1 = half ? c->xbuf + n0 : nullptr;
+  auto conv = [&](bool in) {
+    for (int k = 0; k < 2; ++k) {
+      const size_t n = k ? n1 : n0;
+      if (!n) continue;
+      const int blocks = (int)std::min<size_t>(2048, (n + 1023) / 1024);
+      if (in)
+        hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(blocks), dim3(256), 0, c->cs, k ? b1 : b0,
+                           (long long)n, k ? h1 : h0);
+      else
+        hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(blocks), dim3(256), 0, c->cs, k ? h1 : h0,
+                           (long long)n, k ? b1 : b0);
+      HIP_TRY(hipGetLastError());
+    }
+  };
   {
-    ProfScope ps(c, name, 0, (double)(n0 + n1) * 4.0 + (with_stats ? 8.0 * c->cworld : 0.0));
+    ProfScope ps(c, name, 0,
+                 (double)(n0 + n1) * (half ? 2.0 : 4.0) + (with_stats ? 8.0 * c->cworld : 0.0));
+    if (half) conv(true);
     // the group is closed on every path: a call that fails inside it still
     // runs ncclGroupEnd before the error propagates, so the thread's group
     // depth is back to zero for the caller's next (eager) step
     nccl_try(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
-    if (n0) r = ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs);
-    if (r == ncclSuccess && n1) r = ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs);
+    if (n0)
+      r = half ? ncclAllReduce(h0, h0, n0, ncclBfloat16, ncclSum, c->comm, c->cs)
+               : ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs);
+    if (r == ncclSuccess && n1)
+      r = half ? ncclAllReduce(h1, h1, n1, ncclBfloat16, ncclSum, c->comm, c->cs)
+               : ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs);
     if (r == ncclSuccess && with_stats)
       r = ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs);
     const ncclResult_t re = ncclGroupEnd();
     nccl_try(r);
     nccl_try(re);
+    if (half) conv(false);
   }
   c->cur = prev;
 }
@@ -137,6 +193,8 @@ static void comm_setup(ddpg_ctx* c, int cworld) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)cworld * sizeof(float)));
   if (!c->cs) HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  if (c->cfg.dtype == DDPG_BF16 && !c->xbuf)
+    HIP_TRY(hipMalloc(&c->xbuf, (size_t)c->L.total * sizeof(__bf16)));
   for (auto& ev : c->cev)
     if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 }

@@ -655,8 +655,14 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
 // loads one contiguous run); the Adam state is loaded first so that its
 // round trip overlaps the gradient's.
 constexpr int SB_GU = 16;  // float4s (4 batch rows each) per batch of loads
+// mode 0: gradient + Adam + soft update (+ stats), one launch.  A step with
+// a communicator (data parallelism at small batches) splits it around the
+// RCCL sum of the gradient buffer: mode 1 computes and stores this rank's
+// gradient only (the critic call stores this rank's {max Q, loss share} to
+// g.stats for the all-gather, no running sums); mode 2 reads the summed
+// gradient back and applies Adam, the soft update and the shadow.
 __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTab tab, int net,
-                                                              int nslab) {
+                                                              int nslab, int mode) {
 #ifdef DDPG_SB_STAMPS
   const int sbase = net == 1 ? 48 : 56;
 #endif
@@ -674,11 +680,17 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
   const bool ok = k < T.K && n < T.N;
   const int kc = min(k, T.K - 1), nc = min(n, T.N - 1);
   const size_t i = (size_t)T.off + (size_t)kc * T.N + nc;
-  const float m0 = g.adam_m[i], v0 = g.adam_v[i], p0 = g.theta[i], t0 = g.target[i];
+  float m0 = 0.f, v0 = 0.f, p0 = 0.f, t0 = 0.f;
+  if (mode != 1) {
+    m0 = g.adam_m[i];
+    v0 = g.adam_v[i];
+    p0 = g.theta[i];
+    t0 = g.target[i];
+  }
   const f32x4* xp = T.X ? reinterpret_cast<const f32x4*>(T.X + (size_t)kc * T.ldx) : nullptr;
   const f32x4* dp = reinterpret_cast<const f32x4*>(T.dY + (size_t)nc * T.ldy);
-  const int nq = (g.B + 3) >> 2;
-  float gv = 0.f;
+  const int nq = mode == 2 ? 0 : (g.B + 3) >> 2;
+  float gv = mode == 2 ? g.grad[i] : 0.f;
   for (int q0 = 0; q0 < nq; q0 += SB_GU) {
     f32x4 xv[SB_GU], dv[SB_GU];
 #pragma unroll
@@ -694,7 +706,8 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
         gv = (4 * (q0 + u) + e < g.B) ? fmaf(xv[u][e], dv[u][e], gv) : gv;
   }
   SB_STAMP(sbase + 1);
-  if (ok) {
+  if (ok && mode == 1) g.grad[i] = gv;
+  if (ok && mode != 1) {
     const float alpha = g.alpha[net];
     const float omb1 = __fsub_rn(1.f, g.b1), omb2 = __fsub_rn(1.f, g.b2);
     const float m = __fadd_rn(m0, __fmul_rn(__fsub_rn(gv, m0), omb1));
@@ -704,12 +717,12 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     g.adam_m[i] = m;
     g.adam_v[i] = v;
     g.theta[i] = p;
-    g.grad[i] = gv;
+    if (mode == 0) g.grad[i] = gv;
     g.target[i] = __fadd_rn(__fmul_rn(p, g.tau), __fmul_rn(t0, g.omt));
     if (ti == tab.shadow) tab.sh[(size_t)n * T.K + k] = p;
   }
   SB_STAMP(sbase + 2);
-  if (net == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (net == 1 && mode != 2 && blockIdx.x == 0 && threadIdx.x == 0) {
     float ls = 0.f, qm = -INFINITY;
     for (int w0 = 0; w0 < nslab; w0 += 8) {  // in order, 8 loads in flight
       f32x2v v[8];
@@ -727,9 +740,11 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     const float loss = __fmul_rn(ls, g.inv_b);
     g.stats[0] = qm;
     g.stats[1] = loss;
-    g.acc[0] += (double)qm;
-    g.acc[1] += (double)loss;
-    g.acc[2] += 1.0;
+    if (mode == 0) {  // mode 1: the data-parallel stats reduction keeps the sums
+      g.acc[0] += (double)qm;
+      g.acc[1] += (double)loss;
+      g.acc[2] += 1.0;
+    }
   }
 }
 

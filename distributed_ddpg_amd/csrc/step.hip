@@ -782,6 +782,20 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
 
 // Small-batch learner step: 4 launches (small_batch.h); the gather from the
 // replay ring is fused into the phase kernels (slots already in c->d_slots).
+// With a communicator (data parallelism at the reference's own batch sizes,
+// parameters.py:11,32-34: each rank gathers its slice of the global draw)
+// each network's gradient / Adam kernel runs as two launches around the RCCL
+// sum of that network's flat gradient range: 6 launches + 2 exchanges (the
+// critic's with the stats all-gather), each Adam waiting for its exchange.
+static void sb_wgrad(ddpg_ctx* c, const SbArgs& a, int net, int G, int mode, double nflat) {
+  ProfScope ps(c, mode == 2 ? "sb_adam" : "sb_wgrad_adam", mode == 2 ? 0.0 : 2.0 * a.B * nflat,
+               32.0 * nflat);
+  const SbGradTab& t = c->sb_tab[net];
+  hipLaunchKernelGGL(sb_wgrad_adam_kernel, dim3(t.t[t.n].tile0), dim3(SB_GT), 0, c->cur, a, t,
+                     net, G, mode);
+  HIP_TRY(hipGetLastError());
+}
+
 static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   const Layout& L = c->L;
   const SbArgs a = sb_args(c, rb, B, inv_b);
@@ -789,29 +803,36 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   const long long nc = (long long)(L.critic_end - L.critic_begin);
   const long long na = (long long)(L.actor_end - L.actor_begin);
   const double row_bytes = (2.0 * c->S + c->A + 2) * 4.0;
+  const bool dp = c->comm != nullptr;
+  float* const Gb = c->grad;
   {
     ProfScope ps(c, "sb_phase1", 0, 4.0 * (double)G * (L.total + nc) + B * row_bytes);
     hipLaunchKernelGGL(sb_phase1_kernel, dim3(G * a.xstride), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
-  {
-    ProfScope ps(c, "sb_wgrad_adam", 2.0 * B * nc, 32.0 * nc);
-    const SbGradTab& t = c->sb_tab[1];
-    hipLaunchKernelGGL(sb_wgrad_adam_kernel, dim3(t.t[t.n].tile0), dim3(SB_GT), 0, c->cur, a, t,
-                       1, G);
-    HIP_TRY(hipGetLastError());
+  if (!dp) {
+    sb_wgrad(c, a, 1, G, 0, (double)nc);
+  } else {
+    sb_wgrad(c, a, 1, G, 1, (double)nc);
+    allreduce_on_cs(c, 1, "rccl_allreduce", Gb + L.critic_begin, (size_t)nc, nullptr, 0, true,
+                    nullptr);
+    stats_allreduce_on_cs(c, true);
+    join_cs(c, 2);
+    sb_wgrad(c, a, 1, G, 2, (double)nc);
   }
   {
     ProfScope ps(c, "sb_phase3", 0, 4.0 * (double)G * (L.total + na) + B * c->S * 4.0);
     hipLaunchKernelGGL(sb_phase3_kernel, dim3(G * a.xstride), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
-  {
-    ProfScope ps(c, "sb_wgrad_adam", 2.0 * B * na, 32.0 * na);
-    const SbGradTab& t = c->sb_tab[0];
-    hipLaunchKernelGGL(sb_wgrad_adam_kernel, dim3(t.t[t.n].tile0), dim3(SB_GT), 0, c->cur, a, t,
-                       0, G);
-    HIP_TRY(hipGetLastError());
+  if (!dp) {
+    sb_wgrad(c, a, 0, G, 0, (double)na);
+  } else {
+    sb_wgrad(c, a, 0, G, 1, (double)na);
+    allreduce_on_cs(c, 4, "rccl_allreduce", Gb + L.actor_begin, (size_t)na, nullptr, 0, false,
+                    nullptr);
+    join_cs(c, 5);
+    sb_wgrad(c, a, 0, G, 2, (double)na);
   }
 }
 
@@ -819,8 +840,11 @@ static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B);
 
 // The fused learner step on this step's slots (c->d_slots): the small-batch
 // path (gather fused) or gather + the large-batch GEMM path.
+// world > 1 needs the communicator's exchange (a world > 1 ctx without one
+// -- the rank-slice tests -- stays on the large path, whose unexchanged
+// gradients are that rank's partial sums)
 static bool takes_small(const ddpg_ctx* c, int B) {
-  return c->sb_ok && c->world == 1 && !c->comm && B <= c->sb_max_b;
+  return c->sb_ok && (c->world == 1 || c->comm) && B <= c->sb_max_b;
 }
 
 static void learner_step_any(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
@@ -864,7 +888,8 @@ void sb_setup(ddpg_ctx* c) {
   const int LW = rup(std::max(std::max(c->AH1, c->AH2), std::max(2 * c->CH1, c->CH2)), 4);
   const size_t smem = sb_smem_floats(LX, LW) * sizeof(float);
   // vector weight streams need 4-aligned widths; 160 KiB of LDS per workgroup
-  bool ok = c->world == 1 && hmax <= SB_MAXH && c->AH1 % 4 == 0 && c->AH2 % 4 == 0 &&
+  // (any world: takes_small sends a world > 1 ctx here only with a communicator)
+  bool ok = hmax <= SB_MAXH && c->AH1 % 4 == 0 && c->AH2 % 4 == 0 &&
             c->CH1 % 4 == 0 && c->CH2 % 4 == 0 && smem <= 160 * 1024;
   if (const char* sv = getenv("DDPG_SMALL")) ok = ok && atoi(sv) != 0;
   if (ok) {

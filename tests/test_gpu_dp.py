@@ -277,3 +277,127 @@ def test_ksplit_combine_deterministic_c5_b1024(dd, O, clean_env):
     assert any(k.startswith("gemm_h16i_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
     assert runs[0][1] == runs[1][1]
     _same(runs[0][0], runs[1][0])
+
+
+IP = (4, 1, 128, 200, 3.0)   # InvertedPendulum widths (networks.py:54-55,151-156)
+
+
+def _ip_run(dd, O, p, rows, B, Bg, world=1, comm=None, profile=False, critic_lr=1e-3, steps=1):
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner, Profile, init_comm
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale = IP
+    sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B, world=world,
+                                critic_lr=critic_lr)
+    if comm == "proxy":
+        _lib.check(_lib.lib.ddpg_comm_init_proxy(sess.ctx), sess.ctx)
+    elif comm == "single":
+        init_comm(sess, 0, 1, single=True)
+    rb = ReplayBuffer(len(rows[0]) + 1000, 77)
+    rb.add_batch(*rows)
+    fl = FusedLearner(sess, rb, Bg)
+    prof = Profile(sess)
+    if profile:
+        prof.enable(True)
+    st = [fl.step(stats=True) for _ in range(steps)]
+    keys = sorted(prof.read()) if profile else []
+    if profile:
+        prof.enable(False)
+    out = _state(sess), st, keys, fl.step_counts(), fl.read_stats()
+    sess.close()
+    return out
+
+
+@pytest.mark.parametrize("graph_comm", ["1", "0"])
+def test_small_path_communicator_matches_no_comm(dd, O, clean_env, graph_comm):
+    """Data parallelism at the reference's own shape (InvertedPendulum widths,
+    B = 256 per worker, parameters.py:11,32-34) stays on the small-batch
+    kernels: with a communicator each network's gradient / Adam kernel runs
+    as two launches around the RCCL sum of its gradient range.  Through a
+    1-rank communicator (an identity exchange) three fused steps equal the
+    communicator-less step bitwise -- state, per-step stats and running sums
+    -- replayed from a graph holding the RCCL calls or launched eagerly."""
+    S, A, H1, H2, scale = IP
+    p = _noisy_params(O, S, A, H1, H2, seed=60)
+    rows = _rows(np.random.default_rng(20), 3000, S, A, scale)
+    ref = _ip_run(dd, O, p, rows, 256, 256, steps=3)
+    clean_env.setenv("DDPG_GRAPH_COMM", graph_comm)
+    got = _ip_run(dd, O, p, rows, 256, 256, comm="single", steps=3)
+    assert got[3] == ((3, 0, False) if graph_comm == "1" else (0, 3, False)), got[3]
+    _same(got[0], ref[0])
+    assert got[1] == ref[1]
+    assert got[4] == ref[4]
+    _, _, keys, _, _ = _ip_run(dd, O, p, rows, 256, 256, comm="single", profile=True)
+    for k in ("sb_phase1", "sb_phase3", "sb_wgrad_adam", "sb_adam", "rccl_allreduce", "rccl_stats"):
+        assert k in keys, (k, keys)
+    assert not any(k.startswith("gemm_") for k in keys), keys
+
+
+def test_small_path_proxy_rank0_of_8(dd, O, clean_env):
+    """Rank 0 of an 8-rank data-parallel step at B = 256 per rank (global
+    2048) on the small-batch kernels, proxy communicator: with critic_lr = 0
+    the critic gradient = the oracle's mean over rank 0's slice x 256/2048,
+    the actor gradient = the oracle's batch sum over the slice, the loss
+    share = the slice loss / 8 (1e-4)."""
+    S, A, H1, H2, scale = IP
+    B, Bg, world = 256, 2048, 8
+    p = _noisy_params(O, S, A, H1, H2, seed=61)
+    rows = _rows(np.random.default_rng(21), 5000, S, A, scale)
+    state, st, keys, cnt, _ = _ip_run(dd, O, p, rows, B, Bg, world=world, comm="proxy",
+                                      critic_lr=0.0, profile=True)
+    assert "sb_adam" in keys and "rccl_allreduce" in keys, keys
+    idx = np.array(random.Random(77).sample(range(5000), Bg))[:B]
+    L = O.Learner(S, A, H1, H2, scale, critic_lr=0.0, dtype=np.float64, params=p,
+                  init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    q_max, loss = st[0]
+    assert abs(loss - float(out["loss"]) / world) <= GRAD_TOL * abs(float(out["loss"]) / world)
+    assert abs(q_max - float(np.max(out["q"]))) <= 1e-5 * max(1.0, abs(float(np.max(out["q"]))))
+    for gi, ref, keys_, f in ((9, out["critic_grads"], O.CRITIC_KEYS, 1.0 / world),
+                              (8, out["actor_grads"], O.ACTOR_KEYS, 1.0)):
+        for k, g in zip(keys_, state[gi]):
+            assert rel(g, f * ref[k].reshape(g.shape)) < GRAD_TOL, ("grad", k)
+
+
+def test_proxy_rank0_of_8_c5_bf16_exchange(dd, O, clean_env):
+    """The bf16 configuration at C5 dimensions (S = 376, A = 17, 2048 / 2048)
+    exchanges its gradients as bf16 (one rounding of the rank's fp32
+    gradient, RCCL sum in bf16, widened back for Adam: half the bytes of the
+    fp32 exchange).  Rank 0 of 8 at 512 rows per rank through the proxy
+    communicator, critic_lr = 0: the critic gradient = the oracle's slice
+    mean x 512/4096, the actor gradient = the slice sum, at the stated bf16
+    bars (norm-wise and per-tensor max-rel); the exchanged buffers hold
+    bf16-representable values; the step was a graph replay."""
+    from test_gpu_configs import BF16_GRAD_MAXREL, BF16_GRAD_NORM_TOL, maxrel
+    from test_gpu_parity import normrel
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale = 376, 17, 2048, 2048, 1.0
+    B, Bg, world = 512, 4096, 8
+    p = _noisy_params(O, S, A, H1, H2, seed=62, amp=0.02)
+    rows = _rows(np.random.default_rng(22), 6000, S, A, scale)
+    sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B, world=world,
+                                dtype="bf16", critic_lr=0.0)
+    _lib.check(_lib.lib.ddpg_comm_init_proxy(sess.ctx), sess.ctx)
+    rb = ReplayBuffer(8000, 77)
+    rb.add_batch(*rows)
+    fl = FusedLearner(sess, rb, Bg)
+    q_max, loss = fl.step(stats=True)
+    assert fl.step_counts() == (1, 0, False)
+    state = _state(sess)
+    sess.close()
+    idx = np.array(random.Random(77).sample(range(6000), Bg))[:B]
+    L = O.Learner(S, A, H1, H2, scale, critic_lr=0.0, dtype=np.float64, params=p,
+                  init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    assert abs(loss - float(out["loss"]) / world) <= 2e-2 * abs(float(out["loss"]) / world)
+    for gi, ref, keys_, f in ((9, out["critic_grads"], O.CRITIC_KEYS, 1.0 / world),
+                              (8, out["actor_grads"], O.ACTOR_KEYS, 1.0)):
+        for k, g in zip(keys_, state[gi]):
+            r = f * np.asarray(ref[k], np.float64).reshape(g.shape)
+            assert normrel(g, r) < BF16_GRAD_NORM_TOL, ("grad", k, normrel(g, r))
+            assert maxrel(g, r) < BF16_GRAD_MAXREL, ("grad max-rel", k, maxrel(g, r))
+            g32 = np.asarray(g, np.float32)
+            # exchanged as bf16: the low 16 bits of every fp32 value are zero
+            assert np.all((g32.view(np.uint32) & 0xFFFF) == 0), k
