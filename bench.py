@@ -192,18 +192,23 @@ def exchange_bytes(S, A, H1, H2, elt=4):
             "actor_dW2": elt * H1 * H2, "actor_rest": elt * (ap - H1 * H2)}
 
 
-def exposed_exchange_us(xb, win_c_us, win_a_us, n, eff=RCCL_EFF, small=False):
-    """Exchange time on the critical path of one step: the dWh / dW2
-    all-reduces overlap the measured windows (the compute issued between the
-    exchange and the join), the tail calls are fully exposed.  small: the
-    small-batch path's two calls (one per network, nothing to overlap)."""
+def exposed_exchange_us(xb, win, n, eff=RCCL_EFF, small=False):
+    """Exchange time on the critical path of one step.  Per network the comm
+    stream runs the big call (dWh / dW2) then the tail call; `win` holds the
+    measured windows from issuing each call to the join that Adam waits on
+    (critic / critic_tail, actor / actor_tail): the big call starts at 0, the
+    tail is issued at W - W_tail and starts when both it is issued and the big
+    call is done; what runs past the join is exposed.  small: the small-batch
+    path's two calls (one per network, nothing to overlap)."""
     if small:
         return (allreduce_us(xb["critic_dWh"] + xb["critic_rest"], n, eff) +
                 allreduce_us(xb["actor_dW2"] + xb["actor_rest"], n, eff))
-    t = max(0.0, allreduce_us(xb["critic_dWh"], n, eff) - win_c_us)
-    t += allreduce_us(xb["critic_rest"], n, eff)
-    t += max(0.0, allreduce_us(xb["actor_dW2"], n, eff) - win_a_us)
-    t += allreduce_us(xb["actor_rest"], n, eff)
+    t = 0.0
+    for net, big, rest in (("critic", "critic_dWh", "critic_rest"),
+                           ("actor", "actor_dW2", "actor_rest")):
+        w, wt = win.get(net, 0.0), win.get(net + "_tail", 0.0)
+        tail_start = max(w - wt, allreduce_us(xb[big], n, eff))
+        t += max(0.0, tail_start + allreduce_us(xb[rest], n, eff) - w)
     return t
 
 
@@ -248,8 +253,10 @@ def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
            "model": {"xgmi_link_GBs_per_direction": XGMI_LINK_GBS, "rccl_bus_efficiency": RCCL_EFF,
                      "rccl_latency_us": RCCL_LAT_US, "exchange_bytes": xb,
                      "formula": "step(N) = measured per-rank step (proxy communicator, graph) "
-                                "+ sum over the 4 calls of max(0, T_ar(bytes, N) - overlap "
-                                "window) (small-batch path: its 2 calls, fully exposed); "
+                                "+ per network, the part of its two calls (big, then tail, "
+                                "serialised on the comm stream) that runs past the join, from "
+                                "the measured issue-to-join windows (small-batch path: its 2 "
+                                "calls, fully exposed); "
                                 "T_ar = lat + 2(N-1)/N bytes / ((N-1) link eff); "
                                 "pessimistic: eff halved"},
            "measured_1gpu_updates_s": base_value}
@@ -257,11 +264,9 @@ def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
         rows = {}
         for n in ns:
             m = per_rank_step(cfg_name, device, n, mode, rb, dtype)
-            wc = m["window_us"].get("critic", 0.0)
-            wa = m["window_us"].get("actor", 0.0)
             small = m["path"] == "small-batch kernels"
-            ex = exposed_exchange_us(xb, wc, wa, n, small=small)
-            ex_p = exposed_exchange_us(xb, wc, wa, n, RCCL_EFF / 2, small=small)
+            ex = exposed_exchange_us(xb, m["window_us"], n, small=small)
+            ex_p = exposed_exchange_us(xb, m["window_us"], n, RCCL_EFF / 2, small=small)
             step = m["step_ms"] + ex / 1000.0
             step_p = m["step_ms"] + ex_p / 1000.0
             # strong: global updates/s; weak: batch-B updates processed by all ranks / s

@@ -306,7 +306,7 @@ struct ddpg_ctx {
   int graph_fail = 0;  // a capture with RCCL calls failed on this ctx
   hipStream_t cs = nullptr;
   hipEvent_t cev[8] = {};
-  int win_rec = -1;     // profiling: open exchange-overlap window (prof_recs index)
+  std::vector<int> win_open;  // profiling: open exchange-overlap windows (prof_recs indices)
   int test_cs_spin = 0;  // env DDPG_TEST_CS_SPIN=us (test hook, cs_spin_scale_kernel)
 
   // profiling

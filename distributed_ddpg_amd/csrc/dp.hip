@@ -95,11 +95,11 @@ void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0
   if (!c->comm) return;
   cs_link(c, ev, c->cur, c->cs);
   const hipStream_t prev = c->cur;
-  if (window && c->prof && c->win_rec < 0) {
+  if (window && c->prof) {
     ProfRec rec{window, ev_get(c), ev_get(c), 0.0, (double)n0 * 4.0};
     HIP_TRY(hipEventRecord(rec.e0, prev));
     c->prof_recs.push_back(rec);
-    c->win_rec = (int)c->prof_recs.size() - 1;
+    c->win_open.push_back((int)c->prof_recs.size() - 1);
   }
   c->cur = c->cs;
   if (c->test_cs_spin) {
@@ -176,10 +176,9 @@ void stats_allreduce_on_cs(ddpg_ctx* c, bool gathered) {
 // the consumer stream (c->cur) waits for every collective queued on cs
 void join_cs(ddpg_ctx* c, int ev) {
   if (!c->comm) return;
-  if (c->win_rec >= 0) {  // close the exchange-overlap window on the consumer stream
-    HIP_TRY(hipEventRecord(c->prof_recs[c->win_rec].e1, c->cur));
-    c->win_rec = -1;
-  }
+  for (int w : c->win_open)  // close the exchange-overlap windows on the consumer stream
+    HIP_TRY(hipEventRecord(c->prof_recs[w].e1, c->cur));
+  c->win_open.clear();
   cs_link(c, ev, c->cs, c->cur);
 }
 

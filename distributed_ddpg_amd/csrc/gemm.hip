@@ -319,8 +319,10 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       }
       // bf16 configuration: the 16x16x32-MFMA kernels
       const bool h16 = c->hnp == 1;
-      // fp32 contexts: RK-A GEMMs (forward, dX) on the 16x16x32 form
-      const bool m16 = c->hnp == 3 && AL == L_RK && c->sw.gemm_m16;
+      // fp32 contexts: RK-A GEMMs (forward, dX) on the 16x16x32 form -- unless
+      // K is split in-launch (small-M plan): with 8-16 k-tiles per block the
+      // 32x32x16 form is 1-2 % faster (per-rank C3 B = 512, profiles/r5/)
+      const bool m16 = c->hnp == 3 && AL == L_RK && c->sw.gemm_m16 && !a.kpart;
       char key[112];
       // "/kc": the splits are combined in-launch (small-M plan)
       // DDPG_PROF_SHAPES=1: the shape and split count in the key too

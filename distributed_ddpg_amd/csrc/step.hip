@@ -2,6 +2,7 @@
 // forward, critic train, dQ/da, actor train, Adam + soft update, the fused
 // step (gather, hipGraph capture and replay, the small-batch path) and the
 // 1:1 reference methods of networks.py.  DESIGN.md §1, §4, §5.
+#include <functional>
 #include "ctx.h"
 #include "kernels.h"
 #include "small_batch.h"
@@ -342,8 +343,12 @@ static void fork_to(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
 // nq < 0: run the critic forward here; otherwise it already ran (fused step,
 // concurrently with the target path) and left nq Wo-projection slabs.
 // par: run dWh concurrently with dcat on aux[0].
+// in_window: work issued on the compute stream while the critic's exchange
+// is in flight, before Adam waits for it (the fused data-parallel step puts
+// the online actor forward there: it reads no critic parameter)
 static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq = -1,
-                             bool par = false) {
+                             bool par = false,
+                             const std::function<void()>& in_window = std::function<void()>()) {
   const Layout& L = c->L;
   if (nq < 0) nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr);
   {
@@ -464,9 +469,12 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
     // the rest of the critic ([Ws bs Wa ba] and [bh Wo bo]) behind dWh on the
     // comm stream, then the stats; Adam waits for all of it
     allreduce_on_cs(c, 1, "rccl_allreduce", G + L.critic_begin, L.c[CWH].off - L.critic_begin,
-                    G + L.c[CBH].off, L.critic_end - L.c[CBH].off, true);
+                    G + L.c[CBH].off, L.critic_end - L.c[CBH].off, true, "xwin|critic_tail");
     stats_allreduce_on_cs(c, true);
+    if (in_window) in_window();
     join_cs(c, 2);
+  } else if (in_window) {
+    in_window();
   }
   adam_launch(c, 1, !fused, fused);
 }
@@ -578,7 +586,7 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   reduce_launch(c, "grad_reduce", tab);
   if (c->comm) {  // [W1 b1] and [b2 W3] behind dW2 on the comm stream
     allreduce_on_cs(c, 4, "rccl_allreduce", G + L.actor_begin, L.a[AW2].off - L.actor_begin,
-                    G + L.a[AB2].off, L.actor_end - L.a[AB2].off);
+                    G + L.a[AB2].off, L.actor_end - L.a[AB2].off, false, "xwin|actor_tail");
     join_cs(c, 5);
   }
   adam_launch(c, 0, !fused, fused);
@@ -677,14 +685,24 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   // y = r + gamma (1 - t) Q'(s2, mu') is formed by the critic loss kernel from
   // the target partials now in qpart_t (critic_train_dev, td_nqt)
   c->td_nqt = nqt;
-  // a_outs = actor.predict(s)  ddpg.py:106 (actor params are unchanged until actor.train)
-  c->cur = s2;
-  actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu, l1);
+  // a_outs = actor.predict(s)  ddpg.py:106 (actor params are unchanged until
+  // actor.train).  Data-parallel step on one stream: issued inside the
+  // critic's exchange window instead (it reads no critic parameter), so the
+  // critic's tail all-reduce runs under it rather than in front of Adam.
+  const bool mu_in_window = c->comm && !c->par;
+  auto online_actor_fwd = [&] { actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu, l1); };
+  if (!mu_in_window) {
+    c->cur = s2;
+    online_actor_fwd();
+  }
   // critic.train(s, a, y)  ddpg.py:100: forward now, loss once y is ready
   c->cur = s0;
   const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr, l1 ? 2 : 0);
   fork_to(c, 1, s1, s0);  // join target path (y)
-  critic_train_dev(c, B, inv_b, true, nq, c->par);
+  if (mu_in_window)
+    critic_train_dev(c, B, inv_b, true, nq, c->par, online_actor_fwd);
+  else
+    critic_train_dev(c, B, inv_b, true, nq, c->par);
   // grads = critic.action_gradients(s, a_outs)  ddpg.py:107 (updated critic)
   fork_to(c, 2, s2, s0);  // join online actor forward (h1, h2, o, mu)
   critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);

@@ -104,8 +104,8 @@ def test_small_m_plan_c3_b512(dd, O, clean_env):
     g_state, g_st, _, g_cnt = _c3_run(dd, O, p, rows, B, B)
     e_state, e_st, keys, e_cnt = _c3_run(dd, O, p, rows, B, B, profile=True)
     assert g_cnt == (1, 0, False) and e_cnt == (0, 1, False), (g_cnt, e_cnt)
-    assert any(k.startswith("gemm_h3m_kernel<RK,KR") and k.endswith("/kc") for k in keys), keys
-    assert any(k.startswith("gemm_h3m_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
+    assert any(k.startswith("gemm_h3_kernel<RK,KR") and k.endswith("/kc") for k in keys), keys
+    assert any(k.startswith("gemm_h3_kernel<RK,RK") and k.endswith("/kc") for k in keys), keys
     _same(g_state, e_state)
     assert g_st == e_st
     idx = np.array(random.Random(77).sample(range(6000), B))
