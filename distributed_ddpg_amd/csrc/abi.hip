@@ -156,6 +156,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.thin_k = !env_is("DDPG_THINK", "0");
       c->sw.gemm_h3 = !env_is("DDPG_GEMM_H3", "0");
       c->sw.gemm_m16 = !env_is("DDPG_GEMM_M16", "0");
+      c->sw.nw_fuse = !env_is("DDPG_NW_FUSE", "0");
       if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = atoi(v) == 1;
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
@@ -209,6 +210,17 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
         {&c->slab_Wa, (size_t)c->split_cap_Wa * c->A * c->CH1},
         {&c->slab_Wh, (size_t)c->split_cap_Wh * 2 * c->CH1 * c->CH2},
     };
+    // the narrow weight gradients fused into the dX epilogues (fp32 contexts,
+    // narrow side <= 64): one partial per 128-row tile and row group
+    if (c->hnp == 3) {
+      const size_t mtm = (size_t)ceil_div(B, 128);
+      auto rg = [](int k) { return (size_t)std::max(1, 16 / ((k + 3) / 4)); };
+      if (c->S <= 64) {
+        req.push_back({&c->nw_W1, mtm * rg(c->S) * c->S * c->AH1});
+        req.push_back({&c->nw_Ws, mtm * rg(c->S) * c->S * c->CH1});
+      }
+      if (c->A <= 64) req.push_back({&c->nw_Wa, mtm * rg(c->A) * c->A * c->CH1});
+    }
     size_t tot = 0;
     for (auto& r : req) tot += (r.n + 63) / 64 * 64;
     HIP_TRY(hipMalloc(&c->dact, tot * sizeof(float)));

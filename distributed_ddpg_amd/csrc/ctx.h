@@ -192,6 +192,9 @@ struct ddpg_ctx {
   float2* lpart = nullptr;                    // loss-kernel block partials
   float *ppart_t, *qpart_t;                   // target-path copies (concurrent branch)
   float *slab_W1, *slab_W2, *slab_W3, *slab_Ws, *slab_Wa, *slab_Wh;
+  // per-row-tile partials of the narrow weight gradients fused into the dX
+  // epilogues (GemmEpi.nw_*; null: not fused)
+  float *nw_W1 = nullptr, *nw_Ws = nullptr, *nw_Wa = nullptr;
   // bf16 twins (gemm_h.h operands): hnp planes (0 off, 1 bf16 config, 3 the
   // exact h/m/l split of fp32).  Parameters: theta's twin at wtw, the
   // target's at wtw + hnp * PT (planes PT apart), current while wtw_ok.
@@ -262,6 +265,7 @@ struct ddpg_ctx {
     bool thin_k = true;    // DDPG_THINK=0: the K <= 64 layers on the GEMMs
     bool gemm_h3 = true;   // DDPG_GEMM_H3=0: twin GEMMs with runtime slot addressing (gemm_h_kernel / gemm_h16_kernel)
     bool gemm_m16 = true;  // DDPG_GEMM_M16=0: fp32 contexts on the 32x32x16 gemm_h3_kernel instead of gemm_h3m_kernel
+    bool nw_fuse = true;   // DDPG_NW_FUSE=0: dW1 / dWs / dWa on the skinny kernel instead of the dX epilogues
     int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h (opt-in)
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only

@@ -161,6 +161,50 @@ DDPG_DEV void store_twin(const GemmEpi& e, size_t i, float4 v) {
   store_twin4(e.outh + i, e.h_plane_stride, e.h_planes, v);
 }
 
+// Narrow weight-gradient partial of a staged tile (GemmEpi.nw_*): Vs holds
+// the tile's PR = BM rows of final values, Xs receives the narrow operand's
+// rows.  Thread t: column quad nq = t % (BN / 4), narrow quad iq and row
+// group g from t / (BN / 4); every thread sums its rows r = g, g + RG, ... in
+// order with fp32 FMAs, and stores its 4 x 4 block to slab (by * RG + g).
+template <int PR, int BN, int NT>
+DDPG_DEV void nw_load(const GemmEpi& e, int set, float* Xs, int tid, int m0) {
+  const int K4 = (e.nw_k[set] + 3) >> 2;
+  const f32x4* X = reinterpret_cast<const f32x4*>(e.nw_x[set]);
+  f32x4* X4 = reinterpret_cast<f32x4*>(Xs);
+  const int ld4 = e.nw_ldx[set] >> 2;
+  for (int f = tid; f < PR * K4; f += NT) {
+    const int r = f / K4, q = f - r * K4;
+    X4[f] = X[(size_t)(m0 + r) * ld4 + q];
+  }
+}
+template <int PR, int BN, int NT, int VS_LD>
+DDPG_DEV void nw_partial(const GemmEpi& e, int set, const float* Vs, const float* Xs, int tid,
+                         int n0, int by) {
+  const int K = e.nw_k[set], K4 = (K + 3) >> 2, RG = e.nw_rg[set];
+  constexpr int NQ = BN / 4;
+  const int nq = tid % NQ, rest = tid / NQ;
+  const int iq = rest % K4, g = rest / K4;
+  if (g >= RG) return;
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4* X4 = reinterpret_cast<const f32x4*>(Xs);
+#pragma unroll 4
+  for (int r = g; r < PR; r += RG) {
+    const f32x4 x = X4[r * K4 + iq];
+    const f32x4 v = *reinterpret_cast<const f32x4*>(Vs + r * VS_LD + 4 * nq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(x[i], v[j], acc[i][j]);
+  }
+  float* o = e.nw_out[set] + (size_t)(by * RG + g) * e.nw_slab[set] + n0 + 4 * nq;
+  if (set == 1) o -= e.nw_col1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * iq + i < K) *reinterpret_cast<f32x4*>(o + (size_t)(4 * iq + i) * e.nw_ld[set]) = acc[i];
+}
+
 // ---------------------------------------------------------------- epilogue
 // Accumulator layout (32x32 MFMA, dtype independent on gfx950): lane l holds
 // column l&31 of tile (i, j); register r holds row (r&3) + 8(r>>2) + 4(l>>5).
@@ -214,12 +258,15 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   else  // not used by the learner; the host rejects other combinations
     __builtin_trap();
 
-  if (!outp && !e.outh && !e.colsum && !e.proj_out) return;
+  if (!outp && !e.outh && !e.colsum && !e.proj_out && !e.nw_out[0] && !e.nw_out[1]) return;
 
   constexpr int VS_LD = TC::VS_LD;
   float* Vs = smem;                      // [PR][VS_LD]
   float* Wps = smem + PR * VS_LD;        // [BN][PN]
   float* red = Wps + BN * PROJ_MAX;      // [NT]
+  float* Xs = red + 2 * GNT;             // [PR][<= 64] narrow rows (nw_*, NPASS == 1)
+  const int nws = (e.nw_out[1] && n0 >= e.nw_col1) ? 1 : 0;  // narrow set of this tile
+  const bool nw = NPASS == 1 && e.nw_out[nws] != nullptr;
   const int PN = (e.proj_n + 3) & ~3;
   if (e.proj_out) {
     for (int idx = tid; idx < BN * PN; idx += NT) {
@@ -255,7 +302,9 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           Vs[rl * VS_LD + wn * WC + j * 32 + acc_col<MF>(r, lane)] = acc[i][j][r];
         }
     }
+    if (nw) nw_load<PR, BN, NT>(e, nws, Xs, tid, m0);
     __syncthreads();
+    if (nw) nw_partial<PR, BN, NT, VS_LD>(e, nws, Vs, Xs, tid, n0, by);
     if ((outp || e.outh) && oct) {
       // 8 columns per thread: 16-B stores for the fp32 rows and every twin plane
       constexpr int C8 = BN / 8, RPR8 = NT / C8;

@@ -312,7 +312,8 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3_kernel(GemmHArgs g) {
   ge.N = g.N;
   ge.e = g.e;
   // the whole 128-row tile in one LDS pass (fits the 144-KB staging region)
-  static_assert((BM * (HG_BN + 4) + HG_BN * PROJ_MAX + 2 * GNT) * 4 <= C::SMEM_BYTES, "epilogue LDS");
+  static_assert((BM * (HG_BN + 4) + HG_BN * PROJ_MAX + 2 * GNT + BM * 64) * 4 <= C::SMEM_BYTES,
+                "epilogue LDS (+ the narrow rows of a fused weight gradient)");
   gemm_epilogue<BM, HG_BN, WGN, 32, BM>(acc, smem, ge, tid, n0, m0, ze, bx, by);
   KC_STAMP(3)
 }

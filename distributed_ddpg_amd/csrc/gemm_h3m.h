@@ -289,7 +289,8 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
   ge.M = g.M;
   ge.N = g.N;
   ge.e = g.e;
-  static_assert((BM * (HG_BN + 4) + HG_BN * PROJ_MAX + 2 * GNT) * 4 <= C::SMEM_BYTES, "epilogue LDS");
+  static_assert((BM * (HG_BN + 4) + HG_BN * PROJ_MAX + 2 * GNT + BM * 64) * 4 <= C::SMEM_BYTES,
+                "epilogue LDS (+ the narrow rows of a fused weight gradient)");
   gemm_epilogue<BM, HG_BN, 4, 16, BM>(out, smem, ge, tid, n0, m0, ze, bx, by);
   KC_STAMP(3)
 }

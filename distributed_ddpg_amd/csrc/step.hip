@@ -343,6 +343,31 @@ static void fork_to(ddpg_ctx* c, int ev, hipStream_t from, hipStream_t to) {
 // nq < 0: run the critic forward here; otherwise it already ran (fused step,
 // concurrently with the target path) and left nq Wo-projection slabs.
 // par: run dWh concurrently with dcat on aux[0].
+// Narrow weight gradients fused into a dX epilogue (GemmEpi.nw_*, gemm_common.h):
+// dW1 = s^T dz1 from the dz1 GEMM, dWs = s^T dcat_s and dWa = a^T dcat_a from
+// the dcat GEMM -- the tile's final values times the narrow operand's rows,
+// one fp32 partial per 128-row tile (and row group), summed by grad_reduce.
+// Replaces the skinny launches and the writes of dz1 / dcat nobody else reads.
+// Needs the dX on gemm_h3 / gemm_h3m (one-pass epilogue: fp32 contexts on the
+// twin path), whole 128-row and 128-column tiles, a <= 64-wide narrow side.
+static int nw_rg(int K) { return std::max(1, 16 / ((K + 3) / 4)); }
+static bool nw_ok(ddpg_ctx* c, const float* dx_a, int ld_a, const float* dx_b, int ld_b, int B,
+                  int N, int Kd, const float* x, int ldx, int K, const float* buf) {
+  int kh;
+  return buf && c->sw.nw_fuse && c->hnp == 3 && c->sw.gemm_h3 && B % 128 == 0 &&
+         N % 128 == 0 && K >= 1 && K <= 64 && ldx % 4 == 0 && ((K + 3) & ~3) <= ldx &&
+         aligned16(x) && gemm_h_ok<L_RK, L_RK>(c, dx_a, ld_a, dx_b, ld_b, B, N, Kd, 1, &kh);
+}
+static void nw_set(GemmEpi& e, int set, const float* x, int ldx, int K, float* out, int ld) {
+  e.nw_x[set] = x;
+  e.nw_ldx[set] = ldx;
+  e.nw_k[set] = K;
+  e.nw_ld[set] = ld;
+  e.nw_rg[set] = nw_rg(K);
+  e.nw_out[set] = out;
+  e.nw_slab[set] = (long long)K * ld;
+}
+
 // in_window: work issued on the compute stream while the critic's exchange
 // is in flight, before Adam waits for it (the fused data-parallel step puts
 // the online actor forward there: it reads no critic parameter)
@@ -438,6 +463,21 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   e.ldo = c->ldC;
   e.colsum = c->colpart;
   e.ld_colsum = 2 * c->CH1;
+  // dWs / dWa in the same epilogue when they qualify (nw_ok); dcat is then
+  // written only for a half whose weight gradient still reads it
+  const float* whp = P(c, c->theta, L.c[CWH]);
+  const bool fs = nw_ok(c, c->dhp, c->ldCH2, whp, c->CH2, B, 2 * c->CH1, c->CH2, c->s, c->ldS,
+                        c->S, c->nw_Ws) &&
+                  c->CH1 % 128 == 0;
+  const bool fa = nw_ok(c, c->dhp, c->ldCH2, whp, c->CH2, B, 2 * c->CH1, c->CH2, c->a, c->ldA,
+                        c->A, c->nw_Wa) &&
+                  c->CH1 % 128 == 0;
+  if (fs) nw_set(e, 0, c->s, c->ldS, c->S, c->nw_Ws, c->CH1);
+  if (fa) {
+    nw_set(e, 1, c->a, c->ldA, c->A, c->nw_Wa, c->CH1);
+    e.nw_col1 = c->CH1;
+  }
+  if (fs && fa) e.out = nullptr;
   // one bf16 plane and dWs on the twin GEMM (S > 64, not the skinny kernel):
   // the state half's fp32 values have no reader -- only the action half
   // (dWa on the skinny kernel) is stored in fp32
@@ -447,18 +487,28 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   GemmPlan pdc = gemm_launch<L_RK, L_RK>(c, "dx", c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]),
                                          c->CH2, B, 2 * c->CH1, c->CH2, e);
   const int mt = pdc.mt(B);
-  // dWs = s^T . dcs ; dWa = a^T . dca
-  GemmPlan pWs = wgrad_launch(c, c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, c->slab_Ws,
-                              c->split_cap_Ws, c->grad + L.c[CWS].off);
-  GemmPlan pWa = wgrad_launch(c, c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A, c->CH1, B,
-                              c->slab_Wa, c->split_cap_Wa, c->grad + L.c[CWA].off);
+  // dWs = s^T . dcs ; dWa = a^T . dca  (unless fused above)
+  GemmPlan pWs, pWa;
+  if (!fs)
+    pWs = wgrad_launch(c, c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, c->slab_Ws,
+                       c->split_cap_Ws, c->grad + L.c[CWS].off);
+  if (!fa)
+    pWa = wgrad_launch(c, c->a, c->ldA, c->dcat + c->CH1, c->ldC, c->A, c->CH1, B, c->slab_Wa,
+                       c->split_cap_Wa, c->grad + L.c[CWA].off);
   if (par) fork_to(c, 5, c->aux[0], main);  // join dWh
   // gather every critic gradient into the flat grad buffer
   ReduceTable tab;
   tab.nseg = 0;
-  add_wgrad(tab, pWs, c->slab_Ws, G + L.c[CWS].off, (long long)c->S * c->CH1);
+  const long long nWs = (long long)c->S * c->CH1, nWa = (long long)c->A * c->CH1;
+  if (fs)
+    add_seg(tab, c->nw_Ws, G + L.c[CWS].off, nWs, mt * nw_rg(c->S), nWs);
+  else
+    add_wgrad(tab, pWs, c->slab_Ws, G + L.c[CWS].off, nWs);
   add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, c->CH1);
-  add_wgrad(tab, pWa, c->slab_Wa, G + L.c[CWA].off, (long long)c->A * c->CH1);
+  if (fa)
+    add_seg(tab, c->nw_Wa, G + L.c[CWA].off, nWa, mt * nw_rg(c->A), nWa);
+  else
+    add_wgrad(tab, pWa, c->slab_Wa, G + L.c[CWA].off, nWa);
   add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, c->CH1);
   if (!c->comm) add_wgrad(tab, pWh, c->slab_Wh, G + L.c[CWH].off, nWh);
   add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, c->CH2);
@@ -558,7 +608,8 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
                     "xwin|actor");
   }
   c->cur = main;
-  // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1
+  // dz1 = (dz2 . W2^T) * elu'(h1); colsum -> db1; dW1 = s^T dz1 in the same
+  // epilogue when it qualifies (nw_ok: dz1 then has no reader and is not written)
   float* colpart1 = c->colpart + (size_t)mt2 * c->AH2;
   e = epi_none();
   e.post = 1;
@@ -570,15 +621,29 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   e.ldo = c->ldAH1;
   e.colsum = colpart1;
   e.ld_colsum = c->AH1;
-  GemmPlan pz1 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz2, c->ldAH2, P(c, c->theta, L.a[AW2]),
-                                         c->AH2, B, c->AH1, c->AH2, e);
-  // dW1 = s^T . dz1
-  GemmPlan pW1 = wgrad_launch(c, c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1, B, c->slab_W1,
-                              c->split_cap_W1, G + L.a[AW1].off);
+  const float* w2p = P(c, c->theta, L.a[AW2]);
+  const bool f1 = nw_ok(c, c->dz2, c->ldAH2, w2p, c->AH2, B, c->AH1, c->AH2, c->s, c->ldS, c->S,
+                        c->nw_W1);
+  if (f1) {
+    nw_set(e, 0, c->s, c->ldS, c->S, c->nw_W1, c->AH1);
+    e.out = nullptr;
+    e.outh = nullptr;
+  }
+  GemmPlan pz1 = gemm_launch<L_RK, L_RK>(c, "dx", c->dz2, c->ldAH2, w2p, c->AH2, B, c->AH1,
+                                         c->AH2, e);
+  // dW1 = s^T . dz1  (unless fused above)
+  GemmPlan pW1;
+  if (!f1)
+    pW1 = wgrad_launch(c, c->s, c->ldS, c->dz1, c->ldAH1, c->S, c->AH1, B, c->slab_W1,
+                       c->split_cap_W1, G + L.a[AW1].off);
   if (par) fork_to(c, 3, c->aux[0], main);  // join dW3, dW2
   ReduceTable tab;
   tab.nseg = 0;
-  add_wgrad(tab, pW1, c->slab_W1, G + L.a[AW1].off, (long long)c->S * c->AH1);
+  const long long nW1 = (long long)c->S * c->AH1;
+  if (f1)
+    add_seg(tab, c->nw_W1, G + L.a[AW1].off, nW1, pz1.mt(B) * nw_rg(c->S), nW1);
+  else
+    add_wgrad(tab, pW1, c->slab_W1, G + L.a[AW1].off, nW1);
   add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, pz1.mt(B), c->AH1);
   if (!c->comm) add_wgrad(tab, pW2, c->slab_W2, G + L.a[AW2].off, nW2);
   add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt2, c->AH2);

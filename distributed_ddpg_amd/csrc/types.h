@@ -56,6 +56,18 @@ struct GemmEpi {
   // fp32 `out` stored only for columns n >= out_col0 (the twin for all): an
   // output whose leading columns have twin readers only
   int out_col0;
+  // Narrow weight gradient of the NEXT layer down, from this dX tile (the
+  // input layers' dW1 = s^T dz1, dWs = s^T dcat_s, dWa = a^T dcat_a with a
+  // <= 64-wide narrow side): the tile's final values v (rows m0 .. m0 + BM,
+  // columns n0 .. n0 + BN) times the narrow operand's rows, one partial per
+  // row tile and row group into nw_out[set] + (by * nw_rg + g) * nw_slab
+  // ([nw_k][nw_ld] each; grad_reduce sums the slabs).  Set 1 (if any) takes the
+  // columns n >= nw_col1 (dcat's action half).  One-pass epilogues only.
+  const float* nw_x[2];  // narrow operand [M][nw_ldx], 16-B rows
+  int nw_ldx[2], nw_k[2], nw_ld[2], nw_rg[2];
+  float* nw_out[2];
+  long long nw_slab[2];
+  int nw_col1;
 };
 
 struct GemmArgs {

@@ -36,6 +36,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_THINK=0      the K <= 64 layers on the tiled GEMMs instead of thin_k
     DDPG_SKINNY=0     the <= 64-wide weight gradients on the GEMMs instead of
                       the skinny VALU kernel
+    DDPG_NW_FUSE=0    dW1 / dWs / dWa on the skinny kernel instead of the dz1 /
+                      dcat GEMM epilogues
     DDPG_GEMM_M16=0   the fp32 forward / dX twin GEMMs on gemm_h3_kernel
                       (32x32x16 MFMA) instead of gemm_h3m_kernel (16x16x32:
                       32 products per MFMA instead of 16, fp32 rounding differs)
@@ -60,7 +62,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
-            "DDPG_GEMM_M16")
+            "DDPG_GEMM_M16", "DDPG_NW_FUSE")
 
 
 @pytest.fixture(scope="module")
@@ -159,6 +161,8 @@ def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
         # sides (gemm_h3_kernel vs gemm_h_kernel: same products, same order)
         monkeypatch.setenv("DDPG_KCOMB", "0")
         monkeypatch.setenv("DDPG_GEMM_M16", "0")
+        # the fused narrow weight gradients run in gemm_h3's epilogue only
+        monkeypatch.setenv("DDPG_NW_FUSE", "0")
     p, _ = _params(O, name)
     ref = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
     monkeypatch.setenv(switch, value)
@@ -288,6 +292,50 @@ def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent)
     for (net, keys), vals in zip(nets, got["state"][:4]):
         for k, v in zip(keys, vals):
             assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (switch, net, k))
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_narrow_wgrad_fused_into_dx(dd, O, monkeypatch, fuse):
+    """dW1 = s^T dz1, dWs = s^T dcat_s, dWa = a^T dcat_a (narrow side <= 64)
+    computed in the dz1 / dcat GEMM epilogues (per-row-tile fp32 partials
+    summed by grad_reduce) by default -- one skinny launch per step is left
+    (dW3) -- and on the skinny kernel with DDPG_NW_FUSE=0 (four): both meet
+    the oracle's fp32 bars after 3 fused steps at the 1024-wide config."""
+    _clear(monkeypatch)
+    if fuse == "0":
+        monkeypatch.setenv("DDPG_NW_FUSE", "0")
+    p, _ = _params(O, "wide")
+    got = _run(dd, O, "wide", p, 3)
+    L, L32 = _oracle(O, "wide", p, got["rows"], 3)
+    nets = (("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS))
+    for (net, keys), vals in zip(nets, got["state"][:2]):
+        for k, v in zip(keys, vals):
+            assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (fuse, net, k))
+
+
+def test_narrow_wgrad_launch_counts(dd, O, monkeypatch):
+    """The fused form really ran: per fused step 1 skinny launch by default, 4
+    with DDPG_NW_FUSE=0."""
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    counts = {}
+    for fuse in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_NW_FUSE", fuse)
+        p, _ = _params(O, "wide")
+        S, A, H1, H2, scale, B, _ = CONFIGS["wide"]
+        sess, actor, critic = _session(dd, O, "wide", p)
+        rb = ReplayBuffer(5000, 1234)
+        _fill(rb, S, A, 3000, scale, seed=2)
+        fl = FusedLearner(sess, rb, B)
+        prof = Profile(sess)
+        prof.enable(True)
+        fl.step()
+        keys = prof.read()
+        prof.enable(False)
+        sess.close()
+        counts[fuse] = keys.get("skinny_wgrad_kernel|wgrad", {"launches": 0})["launches"]
+    assert counts == {"1": 1, "0": 4}, counts
 
 
 def test_default_path_uses_skinny_wgrad(dd, O, monkeypatch):
