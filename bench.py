@@ -663,7 +663,7 @@ def main():
                                "MB_per_step": round(v["bytes"] / args.profile_steps / 1e6, 3)}
                            for k, v in by_kernel.items() if k.startswith("rccl")}
     hbm = {}
-    for key in ("adam+soft_update", "adam", "soft_update", "gather"):
+    for key in ("adam+reduce+soft_update", "adam+soft_update", "adam", "soft_update", "gather"):
         if key in by_kernel and by_kernel[key]["ms"] > 0:
             k = by_kernel[key]
             hbm[key] = round(k["bytes"] / (k["ms"] * 1e-3) / 1e9, 1)

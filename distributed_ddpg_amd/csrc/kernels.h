@@ -370,10 +370,13 @@ struct ReduceTable {
 
 // Each block reduces EPB = 256 / SG elements (float4 or scalar) of one
 // segment with SG slab groups (SG = 4, 2 or 1 by the slab count): thread
-// group sg sums slabs sg, sg + SG, ... in order, four loads in flight, and the
-// groups are combined in LDS in a fixed order -- deterministic, and segments
-// with few elements and many slabs (bias partials: 64 slabs of 1024) still
-// put 256 threads on every 64 elements.
+// group sg sums slabs sg, sg + SG, ... in order (eight loads in flight), and
+// the groups are combined in LDS in a fixed order -- deterministic, and
+// segments with few elements and many slabs (bias partials: 32 slabs of
+// 1024, fused narrow weight-gradient partials: 32-128 slabs) still put 256
+// threads on every 64 elements.  slab_partial / slab_groups are shared with
+// the Adam pass that folds the reduction in (adam_reduce_kernel): both give
+// the same sum, bit for bit.
 template <class T>
 DDPG_DEV T rs_add(T a, T b);
 template <>
@@ -383,27 +386,42 @@ DDPG_DEV float4 rs_add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
+__host__ __device__ inline int slab_groups(int nslab) { return nslab >= 4 ? 4 : (nslab >= 2 ? 2 : 1); }
+
+// slabs sg, sg + SG, ... < nslab of element i, summed left to right
+template <class T>
+DDPG_DEV T slab_partial(const T* __restrict__ src, long long i, long long ss, int nslab, int sg,
+                        int SG) {
+  int k = sg;
+  T acc = src[i + k * ss];
+  k += SG;
+  for (; k + 7 * SG < nslab; k += 8 * SG) {
+    T x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = src[i + (k + u * SG) * ss];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = rs_add(acc, x[u]);
+  }
+  for (; k + 3 * SG < nslab; k += 4 * SG) {
+    const T x0 = src[i + k * ss], x1 = src[i + (k + SG) * ss];
+    const T x2 = src[i + (k + 2 * SG) * ss], x3 = src[i + (k + 3 * SG) * ss];
+    acc = rs_add(rs_add(rs_add(rs_add(acc, x0), x1), x2), x3);
+  }
+  for (; k < nslab; k += SG) acc = rs_add(acc, src[i + k * ss]);
+  return acc;
+}
+
 template <class T>
 DDPG_DEV void reduce_seg(const T* __restrict__ src, T* __restrict__ dst, long long n,
                          long long ss, int nslab, T* part) {
-  const int SG = nslab >= 4 ? 4 : (nslab >= 2 ? 2 : 1);
+  const int SG = slab_groups(nslab);
   const int EPB = 256 / SG;
   const int e = threadIdx.x % EPB, sg = threadIdx.x / EPB;
   for (long long i0 = (long long)blockIdx.x * EPB; i0 < n; i0 += (long long)gridDim.x * EPB) {
     const long long i = i0 + e;
     T acc{};
-    if (i < n && sg < SG) {
-      int k = sg;
-      acc = src[i + k * ss];
-      k += SG;
-      for (; k + 3 * SG < nslab; k += 4 * SG) {
-        const T x0 = src[i + k * ss], x1 = src[i + (k + SG) * ss];
-        const T x2 = src[i + (k + 2 * SG) * ss], x3 = src[i + (k + 3 * SG) * ss];
-        acc = rs_add(rs_add(rs_add(rs_add(acc, x0), x1), x2), x3);
-      }
-      for (; k < nslab; k += SG) acc = rs_add(acc, src[i + k * ss]);
-    }
-    if (sg > 0 && sg < SG) part[(sg - 1) * 256 + e] = acc;
+    if (i < n) acc = slab_partial(src, i, ss, nslab, sg, SG);
+    if (sg > 0) part[(sg - 1) * 256 + e] = acc;
     __syncthreads();
     if (sg == 0 && i < n) {
       for (int q = 1; q < SG; ++q) acc = rs_add(acc, part[(q - 1) * 256 + e]);
@@ -439,15 +457,46 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceTable tab) {
 // updated from the new p in the same pass (networks.py:34-37, the same fp32
 // ops as soft_update_kernel; nothing reads the targets between this network's
 // Adam step and the end of the step), ttw its twin.
+// alpha = lr * sqrt(1 - b2p) / (1 - b1p) from a network's beta powers
+DDPG_DEV float adam_alpha(const float* pw, float lr) {
+  return __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.f, pw[1]))), __fsub_rn(1.f, pw[0]));
+}
+
+// The fused learner step's beta-power bookkeeping, folded into its two Adam
+// passes instead of a launch of its own at the end of the step (AdamHooks):
+// the critic's pass (first) computes the actor's step size into a device slot
+// and then advances the actor's powers -- nothing reads them until the next
+// step; the actor's pass (second) takes its step size from that slot and
+// advances the critic's powers, which the critic's pass has consumed.  Same
+// values and ops as adam_alpha + advance_powers_kernel after both passes.
+struct AdamHooks {
+  const float* alpha_in;  // step size from here instead of pw
+  float* pre_pw;          // block 0: *pre_alpha = alpha(pre_pw, pre_lr), then advance pre_pw
+  float* pre_alpha;
+  float pre_lr;
+  float* adv_pw;          // block 0: advance adv_pw
+};
+DDPG_DEV void adam_hooks(const AdamHooks& h, float b1, float b2) {
+  if (blockIdx.x || threadIdx.x) return;
+  if (h.pre_pw) {
+    *h.pre_alpha = adam_alpha(h.pre_pw, h.pre_lr);
+    h.pre_pw[0] = __fmul_rn(h.pre_pw[0], b1);
+    h.pre_pw[1] = __fmul_rn(h.pre_pw[1], b2);
+  }
+  if (h.adv_pw) {
+    h.adv_pw[0] = __fmul_rn(h.adv_pw[0], b1);
+    h.adv_pw[1] = __fmul_rn(h.adv_pw[1], b2);
+  }
+}
+
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ g, long long n,
                             const float* __restrict__ pw, float lr, float b1, float b2,
                             float eps, __bf16* __restrict__ tw, long long tps, int tnp,
                             float* __restrict__ tt, float tau, float omt,
-                            __bf16* __restrict__ ttw) {
-  const float b1p = pw[0], b2p = pw[1];
-  const float alpha = __fdiv_rn(__fmul_rn(lr, __fsqrt_rn(__fsub_rn(1.f, b2p))),
-                                __fsub_rn(1.f, b1p));
+                            __bf16* __restrict__ ttw, AdamHooks hk) {
+  const float alpha = hk.alpha_in ? *hk.alpha_in : adam_alpha(pw, lr);
+  adam_hooks(hk, b1, b2);
   const float omb1 = __fsub_rn(1.f, b1), omb2 = __fsub_rn(1.f, b2);
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -493,6 +542,129 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ m,
       if (ttw) store_twin1(ttw + i, tps, tnp, tt[i]);
     }
   }
+}
+
+// Adam with the network's gradient reduction folded in (no exchange between
+// them: one rank, or no communicator).  The network's flat region is covered
+// by segments: slab segments (the reduce table's, summed exactly as
+// reduce_slabs_kernel sums them, the sum also stored to the flat gradient)
+// and direct ones (the gradient already in place).  Per element the same
+// ApplyAdam / soft-update / twin ops as adam_kernel, so the two forms agree
+// bit for bit.  Blocks [blk0, blk0 + nblk) work on a segment.
+struct AdamSeg {
+  const float* src;
+  long long off;    // flat index of the segment's first element
+  long long count;
+  long long slab_stride;
+  int nslab, vec4, wg, blk0, nblk;
+};
+constexpr int ADAM_MAXSEG = 20;
+struct AdamTable {
+  AdamSeg seg[ADAM_MAXSEG];
+  int nseg;
+};
+struct AdamArgs {
+  float *p, *m, *v, *g;  // flat bases (index = flat element)
+  const float* pw;
+  float lr, b1, b2, eps;
+  __bf16* tw;            // theta's twin (flat base) or null
+  long long tps;
+  int tnp;
+  float* tt;             // targets (fused step) or null
+  float tau, omt;
+  __bf16* ttw;
+  AdamHooks hk;
+};
+
+DDPG_DEV void adam_elem(float& p, float& m, float& v, float g, float alpha, float omb1, float omb2,
+                        float eps) {
+  m = __fadd_rn(m, __fmul_rn(__fsub_rn(g, m), omb1));
+  v = __fadd_rn(v, __fmul_rn(__fsub_rn(__fmul_rn(g, g), v), omb2));
+  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
+}
+
+template <class T>
+DDPG_DEV void adam_apply(const AdamArgs& a, long long j, T G, float alpha, float omb1, float omb2);
+template <>
+DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float4 G, float alpha, float omb1,
+                         float omb2) {
+  float4 P = *reinterpret_cast<float4*>(a.p + j);
+  float4 M = *reinterpret_cast<float4*>(a.m + j);
+  float4 V = *reinterpret_cast<float4*>(a.v + j);
+  adam_elem(P.x, M.x, V.x, G.x, alpha, omb1, omb2, a.eps);
+  adam_elem(P.y, M.y, V.y, G.y, alpha, omb1, omb2, a.eps);
+  adam_elem(P.z, M.z, V.z, G.z, alpha, omb1, omb2, a.eps);
+  adam_elem(P.w, M.w, V.w, G.w, alpha, omb1, omb2, a.eps);
+  *reinterpret_cast<float4*>(a.p + j) = P;
+  *reinterpret_cast<float4*>(a.m + j) = M;
+  *reinterpret_cast<float4*>(a.v + j) = V;
+  if (a.tw) store_twin4(a.tw + j, a.tps, a.tnp, P);
+  if (a.tt) {
+    float4 b = *reinterpret_cast<float4*>(a.tt + j);
+    b.x = __fadd_rn(__fmul_rn(P.x, a.tau), __fmul_rn(b.x, a.omt));
+    b.y = __fadd_rn(__fmul_rn(P.y, a.tau), __fmul_rn(b.y, a.omt));
+    b.z = __fadd_rn(__fmul_rn(P.z, a.tau), __fmul_rn(b.z, a.omt));
+    b.w = __fadd_rn(__fmul_rn(P.w, a.tau), __fmul_rn(b.w, a.omt));
+    *reinterpret_cast<float4*>(a.tt + j) = b;
+    if (a.ttw) store_twin4(a.ttw + j, a.tps, a.tnp, b);
+  }
+}
+template <>
+DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float G, float alpha, float omb1,
+                         float omb2) {
+  float P = a.p[j], M = a.m[j], V = a.v[j];
+  adam_elem(P, M, V, G, alpha, omb1, omb2, a.eps);
+  a.p[j] = P;
+  a.m[j] = M;
+  a.v[j] = V;
+  if (a.tw) store_twin1(a.tw + j, a.tps, a.tnp, P);
+  if (a.tt) {
+    const float b = __fadd_rn(__fmul_rn(P, a.tau), __fmul_rn(a.tt[j], a.omt));
+    a.tt[j] = b;
+    if (a.ttw) store_twin1(a.ttw + j, a.tps, a.tnp, b);
+  }
+}
+
+template <class T>
+DDPG_DEV void adam_seg(const AdamSeg& g, const AdamArgs& a, int lb, T* part, float alpha,
+                       float omb1, float omb2) {
+  constexpr int W = sizeof(T) / sizeof(float);
+  const T* __restrict__ src = reinterpret_cast<const T*>(g.src);
+  const long long n = g.count / W, ss = g.slab_stride / W;
+  const int SG = slab_groups(g.nslab);
+  const int EPB = 256 / SG;
+  const int e = threadIdx.x % EPB, sg = threadIdx.x / EPB;
+  for (long long i0 = (long long)lb * EPB; i0 < n; i0 += (long long)g.nblk * EPB) {
+    const long long i = i0 + e;
+    T acc{};
+    if (i < n) acc = slab_partial(src, i, ss, g.nslab, sg, SG);
+    if (SG > 1) {
+      if (sg > 0) part[(sg - 1) * 256 + e] = acc;
+      __syncthreads();
+    }
+    if (sg == 0 && i < n) {
+      for (int q = 1; q < SG; ++q) acc = rs_add(acc, part[(q - 1) * 256 + e]);
+      const long long j = g.off + i * W;
+      if (g.wg) *reinterpret_cast<T*>(a.g + j) = acc;
+      adam_apply(a, j, acc, alpha, omb1, omb2);
+    }
+    if (SG > 1) __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_reduce_kernel(AdamTable t, AdamArgs a) {
+  __shared__ float4 part[3 * 256];
+  int s = 0;
+  while (s + 1 < t.nseg && (int)blockIdx.x >= t.seg[s + 1].blk0) ++s;
+  const AdamSeg g = t.seg[s];
+  const float alpha = a.hk.alpha_in ? *a.hk.alpha_in : adam_alpha(a.pw, a.lr);
+  adam_hooks(a.hk, a.b1, a.b2);
+  const float omb1 = __fsub_rn(1.f, a.b1), omb2 = __fsub_rn(1.f, a.b2);
+  const int lb = (int)blockIdx.x - g.blk0;
+  if (g.vec4)
+    adam_seg<float4>(g, a, lb, part, alpha, omb1, omb2);
+  else
+    adam_seg<float>(g, a, lb, reinterpret_cast<float*>(part), alpha, omb1, omb2);
 }
 
 // AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2 (fp32),

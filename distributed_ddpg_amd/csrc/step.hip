@@ -303,8 +303,26 @@ static void reduce_launch(ddpg_ctx* c, const char* name, ReduceTable& tab) {
 
 // TF ApplyAdam over one network's flat region.  advance: also advance its
 // beta powers right after (1:1 API path).  soft (fused step): the same pass
-// also soft-updates this network's targets from the new parameters; the
-// fused step then advances both networks' beta powers at its end.
+// also soft-updates this network's targets from the new parameters and does
+// its share of the beta-power bookkeeping (adam_hooks_for).
+// fused learner step: the beta-power bookkeeping rides on the two passes
+// (AdamHooks, kernels.h) -- the critic's pass runs first
+static AdamHooks adam_hooks_for(ddpg_ctx* c, int net, bool fold) {
+  AdamHooks h;
+  memset(&h, 0, sizeof h);
+  if (!fold) return h;
+  float* alpha_slot = c->dpw + 8;
+  if (net == 1) {
+    h.pre_pw = c->dpw;
+    h.pre_alpha = alpha_slot;
+    h.pre_lr = c->cfg.actor_lr;
+  } else {
+    h.alpha_in = alpha_slot;
+    h.adv_pw = c->dpw + 2;
+  }
+  return h;
+}
+
 static void adam_launch(ddpg_ctx* c, int net, bool advance, bool soft = false) {
   const size_t b = net == 0 ? c->L.actor_begin : c->L.critic_begin;
   const size_t e = net == 0 ? c->L.actor_end : c->L.critic_end;
@@ -321,7 +339,89 @@ static void adam_launch(ddpg_ctx* c, int net, bool advance, bool soft = false) {
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, c->cur, c->theta + b,
                        c->adam_m + b, c->adam_v + b, c->grad + b, n, c->dpw + 2 * net, lr,
                        c->cfg.beta1, c->cfg.beta2, c->cfg.epsilon, tw, (long long)c->L.total,
-                       c->hnp, soft ? c->target + b : nullptr, tau, omt, soft ? ttw : nullptr);
+                       c->hnp, soft ? c->target + b : nullptr, tau, omt, soft ? ttw : nullptr,
+                       adam_hooks_for(c, net, soft));
+    HIP_TRY(hipGetLastError());
+  }
+  if (advance) {
+    hipLaunchKernelGGL(advance_powers_kernel, dim3(1), dim3(1), 0, c->cur, c->dpw, 1 << net,
+                       c->cfg.beta1, c->cfg.beta2);
+    HIP_TRY(hipGetLastError());
+  }
+}
+
+// adam_launch with the network's gradient reduction (tab) folded into the
+// same pass: no exchange sits between them (no communicator).  The table's
+// slab segments plus direct segments for the rest of the network's region
+// (gradients already written in place) cover it exactly once.
+static void adam_reduce_launch(ddpg_ctx* c, int net, const ReduceTable& tab, bool advance,
+                               bool soft) {
+  const long long b = (long long)(net == 0 ? c->L.actor_begin : c->L.critic_begin);
+  const long long e = (long long)(net == 0 ? c->L.actor_end : c->L.critic_end);
+  float* G = c->grad;
+  std::vector<const ReduceSeg*> segs;
+  for (int i = 0; i < tab.nseg; ++i) segs.push_back(&tab.seg[i]);
+  std::sort(segs.begin(), segs.end(),
+            [](const ReduceSeg* x, const ReduceSeg* y) { return x->dst < y->dst; });
+  AdamTable t;
+  t.nseg = 0;
+  int blocks = 0;
+  double rbytes = 0;
+  auto add = [&](const float* src, long long off, long long count, long long stride, int nslab,
+                 bool v4) {
+    if (count <= 0) return;
+    if (t.nseg == ADAM_MAXSEG) throw DdpgError(DDPG_EINVAL, "adam_reduce: segment table full");
+    AdamSeg& g = t.seg[t.nseg++];
+    g.src = src;
+    g.off = off;
+    g.count = count;
+    g.slab_stride = stride;
+    g.nslab = nslab;
+    // float4 also needs every flat array (theta, m, v, targets, twins) aligned at off
+    g.vec4 = v4 && count % 4 == 0 && off % 4 == 0 && stride % 4 == 0 && aligned16(src);
+    g.wg = src != G + off;
+    const long long units = g.vec4 ? count / 4 : count;
+    const int epb = 256 / slab_groups(nslab);
+    g.nblk = (int)std::min<long long>(2048, (units + epb - 1) / epb);
+    g.blk0 = blocks;
+    blocks += g.nblk;
+    if (g.wg) rbytes += 4.0 * count * (nslab + 1);
+  };
+  long long cur = b;
+  for (const ReduceSeg* r : segs) {
+    const long long off = (long long)(r->dst - G);
+    if (off < cur || off + r->count > e)
+      throw DdpgError(DDPG_EINVAL, "adam_reduce: gradient segments overlap or leave the network");
+    add(G + cur, cur, off - cur, 0, 1, true);
+    add(r->src, off, r->count, r->slab_stride, r->nslab, r->vec4 != 0);
+    cur = off + r->count;
+  }
+  add(G + cur, cur, e - cur, 0, 1, true);
+  const long long n = e - b;
+  c->sb_shadow_ok = false;
+  AdamArgs a;
+  a.p = c->theta;
+  a.m = c->adam_m;
+  a.v = c->adam_v;
+  a.g = G;
+  a.pw = c->dpw + 2 * net;
+  a.lr = net == 0 ? c->cfg.actor_lr : c->cfg.critic_lr;
+  a.b1 = c->cfg.beta1;
+  a.b2 = c->cfg.beta2;
+  a.eps = c->cfg.epsilon;
+  const bool tw = c->hnp && c->wtw_ok;
+  a.tw = tw ? c->wtw : nullptr;
+  a.tps = (long long)c->L.total;
+  a.tnp = c->hnp;
+  a.tt = soft ? c->target : nullptr;
+  a.tau = c->cfg.tau;
+  a.omt = (float)(1.0 - (double)c->cfg.tau);
+  a.ttw = (soft && tw) ? c->wtw + (size_t)c->hnp * c->L.total : nullptr;
+  a.hk = adam_hooks_for(c, net, soft);
+  {
+    ProfScope ps(c, soft ? "adam+reduce+soft_update" : "adam+reduce", 0,
+                 (soft ? 40.0 : 28.0) * n + rbytes);
+    hipLaunchKernelGGL(adam_reduce_kernel, dim3(blocks), dim3(256), 0, c->cur, t, a);
     HIP_TRY(hipGetLastError());
   }
   if (advance) {
@@ -514,6 +614,10 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   add_seg(tab, part_dbh, G + L.c[CBH].off, c->CH2, nchunk, c->CH2);
   add_seg(tab, part_dWo, G + L.c[CWO].off, c->CH2, nchunk, c->CH2);
   add_seg(tab, part_dbo, G + L.c[CBO].off, 1, nchunk, 1);
+  if (!c->comm) {
+    adam_reduce_launch(c, 1, tab, !fused, fused);
+    return;
+  }
   reduce_launch(c, "grad_reduce", tab);
   if (c->comm) {
     // the rest of the critic ([Ws bs Wa ba] and [bh Wo bo]) behind dWh on the
@@ -648,8 +752,12 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   if (!c->comm) add_wgrad(tab, pW2, c->slab_W2, G + L.a[AW2].off, nW2);
   add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt2, c->AH2);
   add_wgrad(tab, pW3, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A);
+  if (!c->comm) {
+    adam_reduce_launch(c, 0, tab, !fused, fused);
+    return;
+  }
   reduce_launch(c, "grad_reduce", tab);
-  if (c->comm) {  // [W1 b1] and [b2 W3] behind dW2 on the comm stream
+  {  // [W1 b1] and [b2 W3] behind dW2 on the comm stream
     allreduce_on_cs(c, 4, "rccl_allreduce", G + L.actor_begin, L.a[AW2].off - L.actor_begin,
                     G + L.a[AB2].off, L.actor_end - L.a[AB2].off, false, "xwin|actor_tail");
     join_cs(c, 5);
@@ -773,11 +881,8 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);
   // actor.train(s, grads[0])  ddpg.py:109  (forward above reused: same params)
   actor_train_dev(c, B, true, c->par);
-  // actor/critic.update_target_network()  ddpg.py:112-113: done inside each
-  // network's Adam pass above; here both Adam power updates (_finish)
-  hipLaunchKernelGGL(advance_powers_kernel, dim3(1), dim3(1), 0, c->cur, c->dpw, 3,
-                     c->cfg.beta1, c->cfg.beta2);
-  HIP_TRY(hipGetLastError());
+  // actor/critic.update_target_network()  ddpg.py:112-113 and both Adam power
+  // updates (_finish): done inside the two Adam passes above (AdamHooks)
 }
 
 // Rebuild the W^T shadows of the small path after a parameter write outside
