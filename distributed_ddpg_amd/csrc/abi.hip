@@ -210,9 +210,9 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
         {&c->slab_Wa, (size_t)c->split_cap_Wa * c->A * c->CH1},
         {&c->slab_Wh, (size_t)c->split_cap_Wh * 2 * c->CH1 * c->CH2},
     };
-    // the narrow weight gradients fused into the dX epilogues (fp32 contexts,
-    // narrow side <= 64): one partial per 128-row tile and row group
-    if (c->hnp == 3) {
+    // the narrow weight gradients fused into the dX epilogues (twin contexts,
+    // narrow side <= 64): one partial per 128 rows and row group
+    if (c->hnp == 3 || c->hnp == 1) {
       const size_t mtm = (size_t)ceil_div(B, 128);
       auto rg = [](int k) { return (size_t)std::max(1, 16 / ((k + 3) / 4)); };
       if (c->S <= 64) {

@@ -226,14 +226,16 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       ee.h_planes = c->hnp;
     }
   }
-  // the fused narrow weight gradient (nw_*) runs in gemm_h3 / gemm_h3m's
-  // one-pass epilogue only; the caller checked (step.hip nw_ok)
+  // the fused narrow weight gradient (nw_*) runs in the epilogues of gemm_h3 /
+  // gemm_h3m (fp32) and gemm_h16i (bf16, RK A); the caller checked (step.hip nw_ok)
   const bool nwe = e.nw_out[0] || e.nw_out[1];
   // bf16-twin operands (gemm_h.h): both operands twinned, K in whole k-tiles
   int Kh = 0;
   if (gemm_h_ok<AL, BL>(c, A, lda, B, ldb, M, N, K, splits, &Kh)) {
-    if (nwe && !(c->hnp == 3 && c->sw.gemm_h3 && M % 128 == 0 && N % 128 == 0))
-      throw einval("gemm %s: fused narrow weight gradient needs gemm_h3 full tiles", name);
+    if (nwe && !((c->hnp == 3 || (c->hnp == 1 && AL == L_RK)) && c->sw.gemm_h3 &&
+                 M % (c->hnp == 1 ? 256 : 128) == 0 && N % 128 == 0 && splits == 1))
+      throw einval("gemm %s: fused narrow weight gradient needs gemm_h3 / gemm_h16i full tiles",
+                   name);
     const int BKh = c->hnp == 1 ? 64 : 32, BMh = c->hnp == 1 ? 256 : 128;
     const Twin ta = operand_twin(c, A), tb = operand_twin(c, B);
     {

@@ -162,10 +162,12 @@ DDPG_DEV void store_twin(const GemmEpi& e, size_t i, float4 v) {
 }
 
 // Narrow weight-gradient partial of a staged tile (GemmEpi.nw_*): Vs holds
-// the tile's PR = BM rows of final values, Xs receives the narrow operand's
-// rows.  Thread t: column quad nq = t % (BN / 4), narrow quad iq and row
-// group g from t / (BN / 4); every thread sums its rows r = g, g + RG, ... in
-// order with fp32 FMAs, and stores its 4 x 4 block to slab (by * RG + g).
+// PR = 128 rows of final values (the whole tile of gemm_h3 / gemm_h3m, one
+// of the two passes of gemm_h16i's 256-row tile), Xs receives the narrow
+// operand's rows.  Thread t: column quad nq = t % (BN / 4), narrow quad iq
+// and row group g from t / (BN / 4); every thread sums its rows r = g, g +
+// RG, ... in order with fp32 FMAs, and stores its 4 x 4 block to slab
+// (rt * RG + g), rt = the 128-row block's index.
 template <int PR, int BN, int NT>
 DDPG_DEV void nw_load(const GemmEpi& e, int set, float* Xs, int tid, int m0) {
   const int K4 = (e.nw_k[set] + 3) >> 2;
@@ -179,7 +181,7 @@ DDPG_DEV void nw_load(const GemmEpi& e, int set, float* Xs, int tid, int m0) {
 }
 template <int PR, int BN, int NT, int VS_LD>
 DDPG_DEV void nw_partial(const GemmEpi& e, int set, const float* Vs, const float* Xs, int tid,
-                         int n0, int by) {
+                         int n0, int rt) {
   const int K = e.nw_k[set], K4 = (K + 3) >> 2, RG = e.nw_rg[set];
   constexpr int NQ = BN / 4;
   const int nq = tid % NQ, rest = tid / NQ;
@@ -198,7 +200,7 @@ DDPG_DEV void nw_partial(const GemmEpi& e, int set, const float* Vs, const float
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(x[i], v[j], acc[i][j]);
   }
-  float* o = e.nw_out[set] + (size_t)(by * RG + g) * e.nw_slab[set] + n0 + 4 * nq;
+  float* o = e.nw_out[set] + (size_t)(rt * RG + g) * e.nw_slab[set] + n0 + 4 * nq;
   if (set == 1) o -= e.nw_col1;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -264,9 +266,9 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   float* Vs = smem;                      // [PR][VS_LD]
   float* Wps = smem + PR * VS_LD;        // [BN][PN]
   float* red = Wps + BN * PROJ_MAX;      // [NT]
-  float* Xs = red + 2 * GNT;             // [PR][<= 64] narrow rows (nw_*, NPASS == 1)
+  float* Xs = red + 2 * GNT;             // [PR][<= 64] narrow rows (nw_*, PR == 128)
   const int nws = (e.nw_out[1] && n0 >= e.nw_col1) ? 1 : 0;  // narrow set of this tile
-  const bool nw = NPASS == 1 && e.nw_out[nws] != nullptr;
+  const bool nw = PR == 128 && e.nw_out[nws] != nullptr;
   const int PN = (e.proj_n + 3) & ~3;
   if (e.proj_out) {
     for (int idx = tid; idx < BN * PN; idx += NT) {
@@ -302,9 +304,9 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
           Vs[rl * VS_LD + wn * WC + j * 32 + acc_col<MF>(r, lane)] = acc[i][j][r];
         }
     }
-    if (nw) nw_load<PR, BN, NT>(e, nws, Xs, tid, m0);
+    if (nw) nw_load<PR, BN, NT>(e, nws, Xs, tid, m0 + pass * PR);
     __syncthreads();
-    if (nw) nw_partial<PR, BN, NT, VS_LD>(e, nws, Vs, Xs, tid, n0, by);
+    if (nw) nw_partial<PR, BN, NT, VS_LD>(e, nws, Vs, Xs, tid, n0, (m0 + pass * PR) / PR);
     if ((outp || e.outh) && oct) {
       // 8 columns per thread: 16-B stores for the fp32 rows and every twin plane
       constexpr int C8 = BN / 8, RPR8 = NT / C8;

@@ -539,6 +539,9 @@ DDPG_DEV void gemm_h16i_body(const GemmHArgs& g, int z) {
   ge.M = g.M;
   ge.N = g.N;
   ge.e = g.e;
+  static_assert(((BM / 2) * (HG_BN + 4) + HG_BN * PROJ_MAX + 2 * GNT + (BM / 2) * 64) * 4 <=
+                    C::SMEM_BYTES,
+                "epilogue LDS (+ the narrow rows of a fused weight gradient)");
   gemm_epilogue<BM, HG_BN, 4, 16>(out, smem, ge, tid, n0, m0, ze, bx, by);
 }
 

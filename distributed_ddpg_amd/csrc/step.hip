@@ -454,7 +454,8 @@ static int nw_rg(int K) { return std::max(1, 16 / ((K + 3) / 4)); }
 static bool nw_ok(ddpg_ctx* c, const float* dx_a, int ld_a, const float* dx_b, int ld_b, int B,
                   int N, int Kd, const float* x, int ldx, int K, const float* buf) {
   int kh;
-  return buf && c->sw.nw_fuse && c->hnp == 3 && c->sw.gemm_h3 && B % 128 == 0 &&
+  return buf && c->sw.nw_fuse && c->sw.gemm_h3 &&
+         ((c->hnp == 3 && B % 128 == 0) || (c->hnp == 1 && B % 256 == 0)) &&
          N % 128 == 0 && K >= 1 && K <= 64 && ldx % 4 == 0 && ((K + 3) & ~3) <= ldx &&
          aligned16(x) && gemm_h_ok<L_RK, L_RK>(c, dx_a, ld_a, dx_b, ld_b, B, N, Kd, 1, &kh);
 }
@@ -581,9 +582,18 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   // one bf16 plane and dWs on the twin GEMM (S > 64, not the skinny kernel):
   // the state half's fp32 values have no reader -- only the action half
   // (dWa on the skinny kernel) is stored in fp32
+  // (and with dWa fused above, no fp32 half has a reader: the twin alone)
   if (c->hnp == 1 && c->sw.half_twin && c->S > 64 /* SK_NMAX */ && act_twin(c, c->dcat).p &&
-      gemm_h_ok<L_KR, L_KR>(c, c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, 0, &kh))
+      gemm_h_ok<L_KR, L_KR>(c, c->s, c->ldS, c->dcat, c->ldC, c->S, c->CH1, B, 0, &kh)) {
     e.out_col0 = c->CH1;
+    if (fa && !fs) {
+      const Twin t = act_twin(c, c->dcat);
+      e.outh = t.p;
+      e.h_plane_stride = t.ps;
+      e.h_planes = c->hnp;
+      e.out = nullptr;
+    }
+  }
   GemmPlan pdc = gemm_launch<L_RK, L_RK>(c, "dx", c->dhp, c->ldCH2, P(c, c->theta, L.c[CWH]),
                                          c->CH2, B, 2 * c->CH1, c->CH2, e);
   const int mt = pdc.mt(B);
@@ -600,13 +610,14 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   ReduceTable tab;
   tab.nseg = 0;
   const long long nWs = (long long)c->S * c->CH1, nWa = (long long)c->A * c->CH1;
+  // the fused partials: one per 128 batch rows and row group (gemm_common.h)
   if (fs)
-    add_seg(tab, c->nw_Ws, G + L.c[CWS].off, nWs, mt * nw_rg(c->S), nWs);
+    add_seg(tab, c->nw_Ws, G + L.c[CWS].off, nWs, (B / 128) * nw_rg(c->S), nWs);
   else
     add_wgrad(tab, pWs, c->slab_Ws, G + L.c[CWS].off, nWs);
   add_seg(tab, c->colpart, G + L.c[CBS].off, 2 * c->CH1, mt, c->CH1);
   if (fa)
-    add_seg(tab, c->nw_Wa, G + L.c[CWA].off, nWa, mt * nw_rg(c->A), nWa);
+    add_seg(tab, c->nw_Wa, G + L.c[CWA].off, nWa, (B / 128) * nw_rg(c->A), nWa);
   else
     add_wgrad(tab, pWa, c->slab_Wa, G + L.c[CWA].off, nWa);
   add_seg(tab, c->colpart + c->CH1, G + L.c[CBA].off, 2 * c->CH1, mt, c->CH1);
@@ -745,7 +756,7 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   tab.nseg = 0;
   const long long nW1 = (long long)c->S * c->AH1;
   if (f1)
-    add_seg(tab, c->nw_W1, G + L.a[AW1].off, nW1, pz1.mt(B) * nw_rg(c->S), nW1);
+    add_seg(tab, c->nw_W1, G + L.a[AW1].off, nW1, (B / 128) * nw_rg(c->S), nW1);
   else
     add_wgrad(tab, pW1, c->slab_W1, G + L.a[AW1].off, nW1);
   add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, pz1.mt(B), c->AH1);

@@ -104,7 +104,8 @@ def _run(dd, O, name, p, steps, dtype="fp32", seed=2, profile=False, comm=False)
     if profile:
         prof.enable(True)
     st = [fl.step(stats=True) for _ in range(steps)]
-    keys = sorted(prof.read()) if profile else []
+    prof_rows = prof.read() if profile else {}
+    keys = sorted(prof_rows)
     if profile:
         prof.enable(False)
     state = [sess.get_params(w) for w in (_lib.ACTOR, _lib.CRITIC, _lib.ACTOR_TARGET,
@@ -115,7 +116,7 @@ def _run(dd, O, name, p, steps, dtype="fp32", seed=2, profile=False, comm=False)
     acc = fl.read_stats()
     sess.close()
     return {"state": state, "stats": st, "powers": powers, "acc": acc, "keys": keys,
-            "rows": rows}
+            "rows": rows, "prof": prof_rows}
 
 
 def _bitwise(a, b):
@@ -223,9 +224,11 @@ def test_gemm_h3_switch_bf16_bitwise(dd, O, monkeypatch):
     """bf16 configuration: the forward / dX GEMMs on gemm_h16i_kernel (per-tile
     slot base + immediate offsets, gemm_h3.h) by default and on
     gemm_h16_kernel with DDPG_GEMM_H3=0 -- same products in the same order,
-    bitwise equal results after 2 fused steps."""
+    bitwise equal results after 2 fused steps (the narrow weight gradients on
+    the skinny kernel on both sides: gemm_h16_kernel has no fused form)."""
     _clear(monkeypatch)
     monkeypatch.setenv("DDPG_KCOMB", "0")  # gemm_h16_kernel has no in-launch K split
+    monkeypatch.setenv("DDPG_NW_FUSE", "0")
     p, _ = _params(O, "wide")
     ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
     assert any(k.startswith("gemm_h16i_kernel<RK,KR") for k in ref["keys"]), ref["keys"]
@@ -311,6 +314,38 @@ def test_narrow_wgrad_fused_into_dx(dd, O, monkeypatch, fuse):
     for (net, keys), vals in zip(nets, got["state"][:2]):
         for k, v in zip(keys, vals):
             assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (fuse, net, k))
+
+
+def test_narrow_wgrad_fused_bf16(dd, O, monkeypatch):
+    """bf16 configuration with S = 200 > 64, A = 16: dWa = a^T dcat_a in the
+    dcat GEMM's epilogue (gemm_h16i_kernel, two 128-row passes per 256-row
+    tile, one fp32 partial per 128 rows) and dcat then stored as its bf16 twin
+    only (dWs reads the twin); DDPG_NW_FUSE=0: dWa on the skinny kernel from
+    the fp32 dcat.  The same fp32 values summed in another order: the first
+    step's critic gradients agree to 1e-5 norm-wise, one skinny launch per
+    step (dW3) instead of two, and both runs meet the oracle's bf16 bar after
+    3 fused steps."""
+    from test_gpu_parity import BF16_PARAM_TOL, normrel
+    name = "wides"
+    runs = {}
+    for fuse in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_NW_FUSE", fuse)
+        p, _ = _params(O, name)
+        first = _run(dd, O, name, p, 1, dtype="bf16")
+        run = _run(dd, O, name, p, 3, dtype="bf16", profile=True)
+        runs[fuse] = (first, run)
+    L, _ = _oracle(O, name, p, runs["1"][1]["rows"], 3)
+    for u, v in zip(runs["0"][0]["state"][9], runs["1"][0]["state"][9]):  # critic gradients
+        assert normrel(v, u) < 1e-5, normrel(v, u)
+    for fuse, (_, run) in runs.items():
+        for (net, keys), vals in zip((("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS)),
+                                     run["state"][:2]):
+            for k, v in zip(keys, vals):
+                assert rel(v, L.state()[net][k].reshape(v.shape)) < BF16_PARAM_TOL, (fuse, net, k)
+    skinny = {f: sum(v["launches"] for k, v in r["prof"].items()
+                     if k.startswith("skinny_wgrad_kernel")) for f, (_, r) in runs.items()}
+    assert skinny == {"1": 3, "0": 6}, skinny
 
 
 def test_narrow_wgrad_launch_counts(dd, O, monkeypatch):
