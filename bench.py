@@ -238,7 +238,14 @@ def per_rank_step(cfg_name, device, n, mode, rb, dtype, steps=30, warmup=5, prof
                     else "large-batch GEMM path",
             "gpu_busy_ms": round(busy, 4),
             "window_us": {k: round(v, 1) for k, v in win.items()},
-            "kernels_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in top}}
+            "kernels_ms_per_step": {k: round(v["ms"] / prof_steps, 4) for k, v in top},
+            # every call site: [avg us, launches per step]
+            "launches_per_step": sum(v["launches"] for k, v in rows.items()
+                                     if not k.startswith(("rccl", "xwin"))) / prof_steps,
+            "kernels_by_phase": {k: [round(1e3 * v["ms"] / v["launches"], 2),
+                                     v["launches"] / prof_steps]
+                                 for k, v in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])
+                                 if not k.startswith("xwin")}}
 
 
 def projected_scaling(cfg_name, device, rb, dtype, base_value, ns=(2, 4, 8)):
