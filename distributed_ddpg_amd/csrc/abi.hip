@@ -166,6 +166,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.slots_h2d = env_is("DDPG_SLOTS_H2D", "1");
       if (const char* v = getenv("DDPG_TK_RPB")) c->sw.tk_rpb = std::max(0, atoi(v));
       c->sw.kcomb = !env_is("DDPG_KCOMB", "0");
+      c->sw.kc_wgrad = !env_is("DDPG_KCOMB_WGRAD", "0");
       c->sw.tk_fwd = !env_is("DDPG_TK_FWD", "0");
       c->sw.gemm_pack = !env_is("DDPG_GEMM_PACK", "0");
       c->sw.half_twin = !env_is("DDPG_HALF_TWIN", "0");

@@ -282,6 +282,7 @@ struct ddpg_ctx {
     bool gemm_pack = true;   // DDPG_GEMM_PACK=0: deferred GEMMs launched one by one
     bool tk_fwd = true;      // DDPG_TK_FWD=0: thin_k's generic epilogue for forward parts too
     int kc_splits = 4;       // DDPG_KCOMB_SPLITS=s: at most s splits per tile (2 .. KC_MAXS)
+    bool kc_wgrad = true;    // DDPG_KCOMB_WGRAD=0: data-parallel weight gradients keep their slabs
   } sw;
 
   // small-M plan (ksplit_combine, gemm_common.h): kc_rot rotating partial

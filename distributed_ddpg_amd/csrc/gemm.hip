@@ -265,10 +265,20 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       // k-tiles each) and combines the splits in-launch before its epilogue
       // (ksplit_combine).  The immediate-offset kernels only.
       const bool kc_kernel = c->sw.gemm_h3 && (c->hnp == 3 || (c->hnp == 1 && AL == L_RK));
-      if (splits_req == 1 && kc_kernel && c->kc_part) {
+      // data-parallel steps: a split weight gradient with a direct target
+      // combines its splits in-launch too -- the reduced gradient is then
+      // written once, in place, and its all-reduce starts right behind the
+      // GEMM (a one-rank step leaves the slabs to the Adam pass that reads them)
+      const bool kc_wgrad = splits_req != 1 && direct && c->comm && c->hnp == 3 && c->sw.kc_wgrad;
+      if ((splits_req == 1 || (kc_wgrad && (h.splits == 2 || h.splits == 4))) && kc_kernel &&
+          c->kc_part) {
         const int tiles = h.nt(N) * h.mt(M);
         const int nkt = Kh / BKh;
         int sk = std::min({ceil_div(256, tiles), nkt / 3, c->sw.kc_splits});
+        // a weight gradient keeps the slab plan's K ranges: its partials, and
+        // their sum in split order, are then those of the slab reduction
+        // (slab_partial: ((s0 + s1) + s2) + s3), bit for bit
+        if (kc_wgrad) sk = h.splits;
         while (sk > 2 && (size_t)sk * tiles * BMh * HG_BN > c->kc_part_n) --sk;  // partial buffer
         if (tiles < c->sw.kc_blocks && sk >= 2) {
           const int kps = ceil_div(nkt, sk) * BKh;
@@ -279,6 +289,11 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
             a.kticket = c->kc_ticket + (size_t)slot * kKcTickets;
             h.kps = kps;
             h.splits = sk;
+            if (kc_wgrad) {
+              ee.out = direct;
+              ee.out_split_stride = 0;
+              h.direct = true;
+            }
           }
         }
       }
