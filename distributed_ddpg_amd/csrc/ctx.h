@@ -323,7 +323,7 @@ struct ddpg_ctx {
 
 static constexpr int kSlotRing = 4;
 static constexpr int kKcTickets = 1024;  // ticket segment (output tiles) per combined launch
-static constexpr int kHeadRows = 64, kHeadRows4 = 64;
+static constexpr int kHeadRows = 64, kHeadRows4 = 32;
 
 // ---------------------------------------------------------------- profiling helpers
 static hipEvent_t ev_get(ddpg_ctx* c) {
