@@ -221,6 +221,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
         req.push_back({&c->nw_Ws, mtm * rg(c->S) * c->S * c->CH1});
       }
       if (c->A <= 64) req.push_back({&c->nw_Wa, mtm * rg(c->A) * c->A * c->CH1});
+      if (c->A <= 32)
+        req.push_back({&c->tk_dW3, (size_t)ceil_div(B, TK_ROWS) * c->AH2 * c->A});
     }
     size_t tot = 0;
     for (auto& r : req) tot += (r.n + 63) / 64 * 64;

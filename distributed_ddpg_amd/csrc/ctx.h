@@ -195,6 +195,8 @@ struct ddpg_ctx {
   // per-row-tile partials of the narrow weight gradients fused into the dX
   // epilogues (GemmEpi.nw_*; null: not fused)
   float *nw_W1 = nullptr, *nw_Ws = nullptr, *nw_Wa = nullptr;
+  // per-row-tile partials of dW3 fused into thin_k's dz2 launch (TkPart.dw)
+  float* tk_dW3 = nullptr;
   // bf16 twins (gemm_h.h operands): hnp planes (0 off, 1 bf16 config, 3 the
   // exact h/m/l split of fp32).  Parameters: theta's twin at wtw, the
   // target's at wtw + hnp * PT (planes PT apart), current while wtw_ok.

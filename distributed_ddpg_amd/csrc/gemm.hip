@@ -574,6 +574,12 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
     fwd = fwd && full && q.bias && q.act == 1 && q.outh && !q.aux && !q.colsum;
     bwd = bwd && full && !q.bias && q.act == 0 && q.aux && q.colsum && q.ldaux % 4 == 0;
   }
+  // a fused weight gradient (TkPart.dw) needs the aux rows (backward or
+  // generic form) and full row tiles
+  for (int i = 0; i < nparts; ++i)
+    if (a.p[i].dw && !(!fwd && a.p[i].aux && M % TK_ROWS == 0 && a.p[i].dw_k >= 1 &&
+                       a.p[i].dw_k <= a.p[i].K && a.p[i].K <= 32))
+      return 0;
   char key[96];
   snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : bwd ? "<BWD>" : "", name);
   if (c->sw.prof_shapes)
@@ -581,10 +587,16 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
              parts[0].K);
   ProfScope ps(c, key, flops, bytes);
   const dim3 grid(nc, ceil_div(mt, rpb), nparts);
+  bool dw = false;
+  for (int i = 0; i < nparts; ++i) dw = dw || a.p[i].dw;
   if (fwd)
     hipLaunchKernelGGL(thin_k_kernel<1>, grid, dim3(TK_NT), 0, c->cur, a);
+  else if (bwd && dw)
+    hipLaunchKernelGGL((thin_k_kernel<2, true>), grid, dim3(TK_NT), 0, c->cur, a);
   else if (bwd)
     hipLaunchKernelGGL(thin_k_kernel<2>, grid, dim3(TK_NT), 0, c->cur, a);
+  else if (dw)
+    hipLaunchKernelGGL((thin_k_kernel<0, true>), grid, dim3(TK_NT), 0, c->cur, a);
   else
     hipLaunchKernelGGL(thin_k_kernel<0>, grid, dim3(TK_NT), 0, c->cur, a);
   HIP_TRY(hipGetLastError());

@@ -651,13 +651,18 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   const Layout& L = c->L;
   float* G = c->grad;
   const hipStream_t main = c->cur;
-  // dW3 = h2^T . dz3
-  if (par) {
-    fork_to(c, 6, main, c->aux[0]);
-    c->cur = c->aux[0];
+  // dW3 = h2^T . dz3: in the dz2 thin_k launch below, which reads both (fw3,
+  // TkPart.dw), or on its own (the skinny kernel)
+  const bool fw3 = c->tk_dW3 && c->sw.nw_fuse;
+  GemmPlan pW3;
+  if (!fw3) {
+    if (par) {
+      fork_to(c, 6, main, c->aux[0]);
+      c->cur = c->aux[0];
+    }
+    pW3 = wgrad_launch(c, c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, c->slab_W3,
+                       c->split_cap_W3, G + L.a[AW3].off);
   }
-  GemmPlan pW3 = wgrad_launch(c, c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, c->slab_W3,
-                              c->split_cap_W3, G + L.a[AW3].off);
   GemmEpi e = epi_none();
   c->cur = main;
   // dz2 = (dz3 . W3^T) * elu'(h2); colsum -> db2
@@ -683,7 +688,16 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   tp.ldaux = c->ldAH2;
   tp.colsum = c->colpart;
   tp.ld_colsum = c->AH2;
+  if (fw3) {
+    tp.dw = c->tk_dW3;
+    tp.dw_k = c->A;
+    tp.dw_slab = (long long)c->AH2 * c->A;
+  }
   int mt2 = thin_k_launch(c, "dx", &tp, 1, B);
+  const bool w3_fused = fw3 && mt2 > 0;
+  if (fw3 && !w3_fused)
+    pW3 = wgrad_launch(c, c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, c->slab_W3,
+                       c->split_cap_W3, G + L.a[AW3].off);
   if (!mt2) {
     e = epi_none();
     e.post = 1;
@@ -762,7 +776,11 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
   add_seg(tab, colpart1, G + L.a[AB1].off, c->AH1, pz1.mt(B), c->AH1);
   if (!c->comm) add_wgrad(tab, pW2, c->slab_W2, G + L.a[AW2].off, nW2);
   add_seg(tab, c->colpart, G + L.a[AB2].off, c->AH2, mt2, c->AH2);
-  add_wgrad(tab, pW3, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A);
+  if (w3_fused)
+    add_seg(tab, c->tk_dW3, G + L.a[AW3].off, (long long)c->AH2 * c->A, mt2,
+            (long long)c->AH2 * c->A);
+  else
+    add_wgrad(tab, pW3, c->slab_W3, G + L.a[AW3].off, (long long)c->AH2 * c->A);
   if (!c->comm) {
     adam_reduce_launch(c, 0, tab, !fused, fused);
     return;

@@ -64,7 +64,8 @@ DDPG_DEV int tk_oidx(int r, int n) {
 // backward form (dz2 = dz3 . W3^T): no bias, no activation, the EluGrad aux,
 // column sums, full tiles.  thin_k_launch checks; the folded flags and bounds
 // matter because the epilogue row loop is VALU-bound.
-template <int MODE>
+// DW: the fused weight gradient (TkPart.dw) compiled in (MODE != 1).
+template <int MODE, bool DW = false>
 __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
   __shared__ __attribute__((aligned(16))) char lds[TK_LDS];
   char* const wimg = lds;
@@ -296,6 +297,71 @@ __global__ __launch_bounds__(TK_NT) void thin_k_kernel(TkArgs args) {
         P.colsum[(size_t)rt * P.ld_colsum + n0 + tid] = s;
       }
       __syncthreads();
+    }
+    // backward / generic form: the fused weight gradient aux^T X of this row
+    // tile (dW3 = h2^T dz3, networks.py:44's dW beside its dX) on the fp32
+    // MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, an fmaf chain): the aux
+    // rows this thread holds (aq) and the tile's X rows are staged in LDS 32
+    // rows at a time; wave w owns the dw rows (output columns) of 16-column
+    // blocks NBW w .. NBW w + NBW - 1, every 16-wide block of dw's columns;
+    // one fp32 partial per row tile
+    if (DW && MODE != 1 && P.dw) {
+      constexpr int NBW = TK_COLS / 64;         // 16-column blocks per wave
+      float* const Hs = Os;                     // [32][TK_COLS] aux rows
+      float* const Ds = Os + 32 * TK_COLS;      // [32][K] X rows (fp32)
+      const int NAB = (P.dw_k + 15) >> 4;       // 16-wide blocks of dw columns (<= 2)
+      const int li16 = lane & 15, lq = lane >> 4;
+      f32x4 dacc[NBW][2];
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) dacc[b][0] = dacc[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+          const int rl = rg + TK_RG * i;
+          if ((rl >> 5) != half) continue;
+          *reinterpret_cast<f32x4*>(Hs + (rl & 31) * TK_COLS + 8 * c8) = aq[i][0];
+          *reinterpret_cast<f32x4*>(Hs + (rl & 31) * TK_COLS + 8 * c8 + 4) = aq[i][1];
+        }
+        const int K4 = K >> 2;
+        for (int f = tid; f < 32 * K4; f += TK_NT) {
+          const int r = f / K4, q = f - r * K4, m = m0 + 32 * half + r;
+          f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (m < M) v = *reinterpret_cast<const f32x4*>(P.X + (size_t)m * P.ldx + 4 * q);
+          *reinterpret_cast<f32x4*>(Ds + r * K + 4 * q) = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {  // 4 rows per MFMA k-step
+          const int r = 4 * st + lq;
+          float av[NBW], bv[2];
+#pragma unroll
+          for (int b = 0; b < NBW; ++b) av[b] = Hs[r * TK_COLS + (NBW * wave + b) * 16 + li16];
+#pragma unroll
+          for (int ab = 0; ab < 2; ++ab)
+            bv[ab] = (ab < NAB && ab * 16 + li16 < K) ? Ds[r * K + ab * 16 + li16] : 0.f;
+#pragma unroll
+          for (int b = 0; b < NBW; ++b)
+#pragma unroll
+            for (int ab = 0; ab < 2; ++ab)
+              if (ab < NAB)
+                dacc[b][ab] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[b], bv[ab], dacc[b][ab], 0, 0, 0);
+        }
+        __syncthreads();
+      }
+      // D[i][j]: i = dw row (output column) 4 lq + e of the block, j = dw column li16
+#pragma unroll
+      for (int b = 0; b < NBW; ++b)
+#pragma unroll
+        for (int ab = 0; ab < 2; ++ab) {
+          const int a = ab * 16 + li16;
+          if (ab >= NAB || a >= P.dw_k) continue;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int n = n0 + (NBW * wave + b) * 16 + 4 * lq + e;
+            if (n < P.N) P.dw[(size_t)rt * P.dw_slab + (size_t)n * P.dw_k + a] = dacc[b][ab][e];
+          }
+        }
     }
   }
 }

@@ -110,6 +110,12 @@ struct TkPart {
   int hnp;
   float* colsum;      // [row block][ld_colsum] partial column sums of v, or null
   int ld_colsum;
+  // backward form only: the weight gradient aux^T X of the layer whose output
+  // gradient X is (dW3 = h2^T dz3 beside dz2), one fp32 partial per row tile:
+  // dw[rt * dw_slab + n * dw_k + a], a < dw_k <= K <= 32; null: not fused
+  float* dw;
+  int dw_k;
+  long long dw_slab;
 };
 
 constexpr int TK_MAXP = 5;  // parts per launch (blockIdx.z)
@@ -132,6 +138,7 @@ constexpr int TK_XREG = 3 * TK_XIMG > TK_OUT_BYTES ? 3 * TK_XIMG : TK_OUT_BYTES;
 constexpr int TK_LDS = 3 * TK_WIMG + TK_XREG;
 static_assert(TK_LDS <= 80 * 1024, "two blocks per CU");
 static_assert(TK_RG * TK_COLS * 4 <= TK_XREG, "column-sum scratch aliases the output tile");
+static_assert((32 * TK_COLS + 32 * 32) * 4 <= TK_XREG, "fused dW staging aliases the output tile");
 
 // ---------------------------------------------------------------- small-batch path (small_batch.h)
 // Saved per-row tensors that the weight gradients read, feature-major

@@ -36,7 +36,7 @@ def bench_name(rocprof_name):
     if targs is None:
         return sym
     a = [x.strip() for x in targs.split(",")]
-    if sym == "thin_k_kernel" and len(a) == 1:  # MODE: generic / forward / backward form
+    if sym == "thin_k_kernel" and len(a) <= 2:  # MODE (generic / forward / backward form), DW
         return {"0": "thin_k_kernel", "1": "thin_k_kernel<FWD>", "2": "thin_k_kernel<BWD>"}.get(
             a[0], "thin_k_kernel<%s>" % a[0])
     if len(a) < 2:

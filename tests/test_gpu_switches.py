@@ -164,6 +164,8 @@ def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
         monkeypatch.setenv("DDPG_GEMM_M16", "0")
         # the fused narrow weight gradients run in gemm_h3's epilogue only
         monkeypatch.setenv("DDPG_NW_FUSE", "0")
+    if switch == "DDPG_SKINNY_NL":  # the skinny kernel runs only unfused
+        monkeypatch.setenv("DDPG_NW_FUSE", "0")
     p, _ = _params(O, name)
     ref = _run(dd, O, name, p, 3, profile=switch == "DDPG_TK_FWD")
     monkeypatch.setenv(switch, value)
@@ -284,6 +286,8 @@ def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent)
     config still meet the oracle's fp32 bars, on the kernels it names."""
     _clear(monkeypatch)
     monkeypatch.setenv(switch, value)
+    if switch == "DDPG_SKINNY":  # every narrow weight gradient is fused by default
+        monkeypatch.setenv("DDPG_NW_FUSE", "0")
     name = "wide"
     p, _ = _params(O, name)
     got = _run(dd, O, name, p, 3, profile=True)
@@ -301,9 +305,10 @@ def test_kernel_switch_oracle(dd, O, monkeypatch, switch, value, kernel, absent)
 def test_narrow_wgrad_fused_into_dx(dd, O, monkeypatch, fuse):
     """dW1 = s^T dz1, dWs = s^T dcat_s, dWa = a^T dcat_a (narrow side <= 64)
     computed in the dz1 / dcat GEMM epilogues (per-row-tile fp32 partials
-    summed by grad_reduce) by default -- one skinny launch per step is left
-    (dW3) -- and on the skinny kernel with DDPG_NW_FUSE=0 (four): both meet
-    the oracle's fp32 bars after 3 fused steps at the 1024-wide config."""
+    summed with the other slabs) and dW3 = h2^T dz3 in the dz2 thin_k launch
+    by default, and on the skinny kernel with DDPG_NW_FUSE=0 (four launches):
+    both meet the oracle's fp32 bars after 3 fused steps at the 1024-wide
+    config."""
     _clear(monkeypatch)
     if fuse == "0":
         monkeypatch.setenv("DDPG_NW_FUSE", "0")
@@ -322,9 +327,9 @@ def test_narrow_wgrad_fused_bf16(dd, O, monkeypatch):
     tile, one fp32 partial per 128 rows) and dcat then stored as its bf16 twin
     only (dWs reads the twin); DDPG_NW_FUSE=0: dWa on the skinny kernel from
     the fp32 dcat.  The same fp32 values summed in another order: the first
-    step's critic gradients agree to 1e-5 norm-wise, one skinny launch per
-    step (dW3) instead of two, and both runs meet the oracle's bf16 bar after
-    3 fused steps."""
+    step's critic gradients agree to 1e-5 norm-wise, no skinny launch (dW3 in
+    the dz2 thin_k launch) instead of two per step, and both runs meet the
+    oracle's bf16 bar after 3 fused steps."""
     from test_gpu_parity import BF16_PARAM_TOL, normrel
     name = "wides"
     runs = {}
@@ -345,12 +350,13 @@ def test_narrow_wgrad_fused_bf16(dd, O, monkeypatch):
                 assert rel(v, L.state()[net][k].reshape(v.shape)) < BF16_PARAM_TOL, (fuse, net, k)
     skinny = {f: sum(v["launches"] for k, v in r["prof"].items()
                      if k.startswith("skinny_wgrad_kernel")) for f, (_, r) in runs.items()}
-    assert skinny == {"1": 3, "0": 6}, skinny
+    assert skinny == {"1": 0, "0": 6}, skinny
 
 
 def test_narrow_wgrad_launch_counts(dd, O, monkeypatch):
-    """The fused form really ran: per fused step 1 skinny launch by default, 4
-    with DDPG_NW_FUSE=0."""
+    """The fused forms really ran: per fused step no skinny launch by default
+    (dW1 / dWs / dWa in the dX GEMM epilogues, dW3 in the dz2 thin_k launch),
+    4 with DDPG_NW_FUSE=0."""
     from distributed_ddpg_amd.learner import FusedLearner, Profile
     from distributed_ddpg_amd.replay_buffer import ReplayBuffer
     counts = {}
@@ -370,13 +376,15 @@ def test_narrow_wgrad_launch_counts(dd, O, monkeypatch):
         prof.enable(False)
         sess.close()
         counts[fuse] = keys.get("skinny_wgrad_kernel|wgrad", {"launches": 0})["launches"]
-    assert counts == {"1": 1, "0": 4}, counts
+    assert counts == {"1": 0, "0": 4}, counts
 
 
 def test_default_path_uses_skinny_wgrad(dd, O, monkeypatch):
     """The <= 64-wide weight gradients (dW1, dWs, dWa, dW3 at S = 64, A = 16)
-    run on skinny_wgrad_kernel by default, and the 3-step oracle bars hold."""
+    run on skinny_wgrad_kernel when not fused into their producers
+    (DDPG_NW_FUSE=0), and the 3-step oracle bars hold."""
     _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_NW_FUSE", "0")
     p, _ = _params(O, "wide")
     got = _run(dd, O, "wide", p, 3, profile=True)
     assert "skinny_wgrad_kernel|wgrad" in got["keys"], got["keys"]
