@@ -341,10 +341,14 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       }
       // bf16 configuration: the 16x16x32-MFMA kernels
       const bool h16 = c->hnp == 1;
-      // fp32 contexts: RK-A GEMMs (forward, dX) on the 16x16x32 form -- unless
-      // K is split in-launch (small-M plan): with 8-16 k-tiles per block the
-      // 32x32x16 form is 1-2 % faster (per-rank C3 B = 512, profiles/r5/)
-      const bool m16 = c->hnp == 3 && AL == L_RK && c->sw.gemm_m16 && !a.kpart;
+      // fp32 contexts on the 16x16x32 form: the forward / dX GEMMs unless K is
+      // split in-launch (small-M plan: with 8-16 k-tiles per block the
+      // 32x32x16 form is 1-2 % faster, per-rank C3 B = 512, profiles/r5/), and
+      // the weight gradients (KR x KR) always -- a data-parallel step's
+      // in-launch combine then sums the same per-split partials as the
+      // one-rank step's slabs
+      const bool m16 = c->hnp == 3 && c->sw.gemm_m16 &&
+                       ((AL == L_RK && !a.kpart) || (AL == L_KR && BL == L_KR));
       char key[112];
       // "/kc": the splits are combined in-launch (small-M plan)
       // DDPG_PROF_SHAPES=1: the shape and split count in the key too
@@ -379,9 +383,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       } else if (h16)
         hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, c->cur, a);
       else if (c->sw.gemm_h3 && m16) {
-        // the same six plane products on the 16x16x32 MFMA (gemm_h3m.h), RK A operands
-        if constexpr (AL == L_RK)
-          hipLaunchKernelGGL((gemm_h3m_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
+        // the same six plane products on the 16x16x32 MFMA (gemm_h3m.h)
+        hipLaunchKernelGGL((gemm_h3m_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);
       } else if (c->sw.gemm_h3)
         // the same kernel with immediate-offset addressing (gemm_h3.h)
         hipLaunchKernelGGL((gemm_h3_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);

@@ -121,6 +121,21 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
     for (int x = 0; x < NBB; ++x)
       bbase[reg][x] = bo + (BL == L_RK ? rk_pat(wn * 32) : kr_pat(wn * 32 + 16 * (x >> 1), x & 1));
   }
+  // KR operands (the weight gradient's KR x KR) hold 2 TA + 2 TB per-lane
+  // bases per region; the slot-2 region's are the slots-0-1 region's plus a
+  // constant (2 slots), added at the read (an asm add the compiler cannot
+  // hoist back into long-lived registers) -- 12 VGPRs fewer at the 256 limit
+  auto kr_base = [&](unsigned b, auto reg_c, auto add_c) -> unsigned {
+    constexpr int REG = decltype(reg_c)::value;
+    constexpr unsigned ADD = decltype(add_c)::value;
+    if constexpr (REG == 0) {
+      return b;
+    } else {
+      unsigned r;
+      asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "n"(ADD), "v"(b));
+      return r;
+    }
+  };
   // read group J (of NP (TA + TB)) from slot SL: plane J / 6, fragment
   // J % 6 (0 .. TB-1: B fragment, then the A fragments)
   auto read_one = [&](auto sl_c, auto j_c, bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
@@ -134,8 +149,10 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
       if constexpr (BL == L_RK) {
         bv[P][F] = b128_read_off<OFF + F * 16 * (2 * BK)>(bbase[REG][0]);
       } else {
-        bv[P][F] = __builtin_shufflevector(tr_read_off<OFF>(bbase[REG][2 * F]),
-                                           tr_read_off<OFF>(bbase[REG][2 * F + 1]), 0, 1, 2, 3,
+        using RC = std::integral_constant<int, REG>;
+        using AC = std::integral_constant<unsigned, 2u * BSLOT>;
+        bv[P][F] = __builtin_shufflevector(tr_read_off<OFF>(kr_base(bbase[0][2 * F], RC{}, AC{})),
+                                           tr_read_off<OFF>(kr_base(bbase[0][2 * F + 1], RC{}, AC{})), 0, 1, 2, 3,
                                            4, 5, 6, 7);
       }
     } else {
@@ -144,8 +161,10 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
       if constexpr (AL == L_RK) {
         av[P][I] = b128_read_off<OFF + I * 16 * (2 * BK)>(abase[REG][0]);
       } else {
-        av[P][I] = __builtin_shufflevector(tr_read_off<OFF>(abase[REG][2 * I]),
-                                           tr_read_off<OFF>(abase[REG][2 * I + 1]), 0, 1, 2, 3,
+        using RC = std::integral_constant<int, REG>;
+        using AC = std::integral_constant<unsigned, 2u * ASLOT>;
+        av[P][I] = __builtin_shufflevector(tr_read_off<OFF>(kr_base(abase[0][2 * I], RC{}, AC{})),
+                                           tr_read_off<OFF>(kr_base(abase[0][2 * I + 1], RC{}, AC{})), 0, 1, 2, 3,
                                            4, 5, 6, 7);
       }
     }

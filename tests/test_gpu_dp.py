@@ -165,7 +165,7 @@ def test_proxy_rank0_of_8_c3(dd, O, clean_env):
     assert any(k.startswith("xwin|") for k in keys), keys
     # the weight gradients' K splits combined in-launch (no slab reduction in
     # front of their all-reduce)
-    assert any(k.startswith("gemm_h3_kernel<KR,KR") and k.endswith("/kc") for k in keys), keys
+    assert any(k.startswith("gemm_h3m_kernel<KR,KR") and k.endswith("/kc") for k in keys), keys
     _same(g_state, e_state)
     assert g_st == e_st
     idx = np.array(random.Random(77).sample(range(9000), Bg))[:B]
