@@ -401,7 +401,9 @@ def test_single_rank_communicator_matches_no_communicator(dd, O, monkeypatch):
     actor's dW2 then the rest, all on the comm stream) with a 1-rank
     communicator is an identity: gradients, Adam slots, parameters, stats and
     the running sums equal the communicator-less step BITWISE.  B = 1024 keeps
-    both runs on the large-batch path (a communicator always takes it)."""
+    both runs on the large-batch path (a communicator always takes it).  The
+    communicator run combines its weight gradients' K splits in-launch, the
+    other sums the same splits as slabs inside its Adam passes."""
     _clear(monkeypatch)
     name = "wide"
     p, _ = _params(O, name)
@@ -414,6 +416,9 @@ def test_single_rank_communicator_matches_no_communicator(dd, O, monkeypatch):
         del CONFIGS["wide_b1024"]
     assert not any(k.startswith("rccl") for k in ref["keys"]), ref["keys"]
     assert "rccl_allreduce" in got["keys"] and "rccl_stats" in got["keys"], got["keys"]
+    assert any(k.endswith("wgrad/kc") for k in got["keys"]), got["keys"]
+    assert not any(k.endswith("wgrad/kc") for k in ref["keys"]), ref["keys"]
+    assert "adam+reduce+soft_update" in ref["keys"], ref["keys"]
     _bitwise(got, ref)
 
 
