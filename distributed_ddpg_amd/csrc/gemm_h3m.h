@@ -217,6 +217,14 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
     static_for<NMF>([&](auto q_c) {
       constexpr int q = decltype(q_c)::value;
       mfma_q(q_c, av, bv);
+#ifdef H3M_RSPAN  // reads spread over the first H3M_RSPAN gaps (bench knob)
+      static_for<NRG>([&](auto j_c) {
+        constexpr int J = decltype(j_c)::value;
+        if constexpr (J * H3M_RSPAN / NRG == q) {
+          if (nx) read_one(std::integral_constant<int, (SL + 1) % 3>{}, j_c, nav, nbv);
+        }
+      });
+#else
       static_for<RPG>([&](auto r_c) {
         constexpr int J = RPG * q + decltype(r_c)::value;
         if constexpr (J < NRG) {
@@ -225,6 +233,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
                      nav, nbv);
         }
       });
+#endif
       if constexpr (q >= DG0 && (q - DG0) % DGS == 0 && (q - DG0) / DGS < C::G) {
         if (st) piece(t + 3, sl_c, (q - DG0) / DGS);
       }

@@ -1,0 +1,198 @@
+// Microbenchmark (tuning aid, not product code): how much of the NP = 3 twin
+// GEMM's clock the LDS fragment reads cost under the chip's power limit, and
+// whether a 64 x 64 wave tile (a third fewer fragment bytes per MFMA) would
+// hold a higher clock than gemm_h3m's 64 x 32.  One block per CU (256
+// blocks), v_mfma_f32_16x16x32_bf16 with the six plane products; per k-tile
+// and SIMD the same 96 MFMAs (786,432 x 2 flop) in every mode:
+//   mode 0: 8 waves x 64x32 wave tile, operands in registers (no LDS reads)
+//   mode 1: 8 waves x 64x32, 18 fragment reads (ds_read_b128) per wave and tile
+//   mode 2: 4 waves x 64x64, 24 fragment reads per wave and tile
+//   mode 3: mode 1 with the reads in the tile's first 18 MFMA gaps (gemm_h3m's placement)
+// Prints us per launch, TF-eq and the in-kernel clock (s_memtime / s_memrealtime).
+//   hipcc -O3 --offload-arch=gfx950 tools/mfma_lds_power_bench.hip -o tools/mfma_lds_power_bench
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                                       \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+// fragment read R (of 3 * (4 + TB)) goes before MFMA M when R * NMF / NRD == M
+// (spread over the tile), or when R == M (FRONT: gemm_h3m's placement)
+template <int TB, bool FRONT, int M, int R>
+__device__ __forceinline__ void rd_step(bf16x8 (&na)[3][4], bf16x8 (&nb)[3][TB], unsigned lbase) {
+  constexpr int NMF = 6 * 4 * TB, NRD = 3 * (4 + TB);
+  if constexpr (R < NRD) {
+    if constexpr ((FRONT ? R : R * NMF / NRD) == M) {
+      constexpr int p = R / (4 + TB), f = R % (4 + TB);
+      if constexpr (f < 4)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(na[p][f]) : "v"(lbase), "n"(R * 1024));
+      else
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(nb[p][f - 4]) : "v"(lbase), "n"(R * 1024));
+    }
+    rd_step<TB, FRONT, M, R + 1>(na, nb, lbase);
+  }
+}
+
+// MFMA M of the tile's 6 * 4 * TB (product-outer: 4 * TB independent MFMAs
+// between dependent ones), accumulators pinned in AGPRs (the compiler's own
+// allocation shuffles them through VGPRs at 4 x 4 blocks)
+template <int TB, bool READ, bool FRONT, int M>
+__device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
+                                        bf16x8 (&na)[3][4], bf16x8 (&nb)[3][TB],
+                                        f32x4 (&acc)[4][TB], f32x4 (&acs)[4][TB], unsigned lbase) {
+  constexpr int NMF = 6 * 4 * TB;
+  if constexpr (M < NMF) {
+    constexpr int q = M / (4 * TB), i = (M / TB) % 4, j = M % TB;
+    constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+    if constexpr (READ) rd_step<TB, FRONT, M, 0>(na, nb, lbase);
+    if constexpr (q < 5)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                   : "+a"(acs[i][j]) : "v"(fa[PA[q]][i]), "v"(fb[PB[q]][j]));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                   : "+a"(acc[i][j]) : "v"(fa[PA[q]][i]), "v"(fb[PB[q]][j]));
+    mm_step<TB, READ, FRONT, M + 1>(fa, fb, na, nb, acc, acs, lbase);
+  }
+}
+
+// TB 16-column B fragments, 4 16-row A fragments per wave; READ: reload every
+// fragment from LDS each tile (else keep the registers)
+template <int TB, bool READ, bool FRONT = false>
+__global__ __launch_bounds__(TB == 2 ? 512 : 256, 1) void loop(const bf16x8* __restrict__ src,
+                                                               int ntiles, float* out,
+                                                               unsigned long long* clk) {
+  constexpr int NT = TB == 2 ? 512 : 256;
+  constexpr int NF = 3 * (4 + TB);  // fragments per wave and tile
+  __shared__ bf16x8 lds[NF * 64 * (NT / 64)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bf16x8 a[3][4], b[3][TB];
+  for (int i = tid; i < NF * NT; i += NT) lds[i] = src[i % (18 * 512)];
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[p][i] = lds[(wave * NF + p * (4 + TB) + i) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < TB; ++j) b[p][j] = lds[(wave * NF + p * (4 + TB) + 4 + j) * 64 + lane];
+  }
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+  f32x4 acc[4][TB], acs[4][TB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TB; ++j) acc[i][j] = acs[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wslot = (wave * NF) * 64 + lane;
+  // accumulators pinned in AGPRs (the compiler's own allocation shuffles
+  // them through VGPRs at 4 x 4 blocks); product-outer order keeps 4*TB
+  // independent MFMAs between dependent ones
+  // READ: double-buffered like the product kernel: tile t+1's fragments are
+  // read (hand-issued ds_read_b128, spread evenly between tile t's MFMAs so
+  // the 15-deep lgkmcnt never stalls the MFMA chain) and waited for at the
+  // tile's end.  The same slot every tile: the LDS traffic, not the data,
+  // is measured.
+  const unsigned lbase = (unsigned)(size_t)&lds[wslot];  // fragment r at + r KiB
+  auto mm_ld = [&](bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB], bf16x8 (&na)[3][4],
+                   bf16x8 (&nb)[3][TB]) {
+    mm_step<TB, READ, FRONT, 0>(fa, fb, na, nb, acc, acs, lbase);
+    if constexpr (READ) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  bf16x8 a2[3][4], b2[3][TB];
+  for (int t = 0; t < ntiles; t += 2) {
+    mm_ld(a, b, a2, b2);
+    __builtin_amdgcn_s_barrier();
+    mm_ld(READ ? a2 : a, READ ? b2 : b, a, b);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (!READ) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        for (int j = 0; j < TB; ++j) asm volatile("" : "+v"(b[p][j]));
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[p][i]));
+      }
+    }
+  }
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+  float sum = 0.f;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < TB; ++j)
+      for (int r = 0; r < 4; ++r) sum += acc[i][j][r] + acs[i][j][r];
+  out[blockIdx.x * NT + tid] = sum;
+  if (tid == 0) {
+    clk[2 * blockIdx.x] = r1 - r0;
+    clk[2 * blockIdx.x + 1] = c1 - c0;
+  }
+}
+
+int main() {
+  const int nb = 256, ntiles = 2000;
+  std::vector<unsigned short> h(18 * 512 * 8);
+  srand(3);
+  for (size_t i = 0; i < h.size(); ++i) {
+    const int plane = (int)((i / (512 * 8)) % 3);
+    const unsigned sign = rand() & 1, man = rand() & 127;
+    const unsigned ex = 127 - 8 * plane - (rand() & 3);
+    h[i] = (unsigned short)((sign << 15) | (ex << 7) | man);
+  }
+  bf16x8* src;
+  float* out;
+  unsigned long long* clk;
+  CHECK(hipMalloc(&src, h.size() * 2));
+  CHECK(hipMalloc(&out, nb * 512 * 4));
+  CHECK(hipMalloc(&clk, nb * 2 * 8));
+  CHECK(hipMemcpy(src, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  static const char* names[4] = {"8 waves 64x32, registers   ", "8 waves 64x32, 18 reads/tile",
+                                 "4 waves 64x64, 24 reads/tile", "8 waves 64x32, 18 front-read"};
+  for (int round = 0; round < 3; ++round) {
+    for (int mode = 0; mode < 4; ++mode) {
+      auto launch = [&]() {
+        if (mode == 0)
+          hipLaunchKernelGGL((loop<2, false>), dim3(nb), dim3(512), 0, 0, src, ntiles, out, clk);
+        else if (mode == 1)
+          hipLaunchKernelGGL((loop<2, true>), dim3(nb), dim3(512), 0, 0, src, ntiles, out, clk);
+        else if (mode == 2)
+          hipLaunchKernelGGL((loop<4, true>), dim3(nb), dim3(256), 0, 0, src, ntiles, out, clk);
+        else
+          hipLaunchKernelGGL((loop<2, true, true>), dim3(nb), dim3(512), 0, 0, src, ntiles, out, clk);
+      };
+      for (int i = 0; i < 3; ++i) launch();
+      CHECK(hipDeviceSynchronize());
+      const int reps = 10;
+      CHECK(hipEventRecord(e0));
+      for (int i = 0; i < reps; ++i) launch();
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      std::vector<unsigned long long> c(nb * 2);
+      CHECK(hipMemcpy(c.data(), clk, c.size() * 8, hipMemcpyDeviceToHost));
+      double ghz = 0, cyc = 0;
+      for (int b = 0; b < nb; ++b) {
+        ghz += (double)c[2 * b + 1] / (double)c[2 * b] / 10.0;
+        cyc += (double)c[2 * b + 1];
+      }
+      const double us = 1e3 * ms / reps;
+      // per block and tile: 8 waves x 48 or 4 waves x 96 MFMAs of 16x16x32 = 16384 flop each
+      const double fl = (double)nb * 384 * ntiles * 16384.0 / 6.0;  // fp32-eq flop
+      printf("round %d %s: %8.1f us/launch, %6.1f TF-eq (%.3f of 417), %.0f cyc/tile (MFMA-bound "
+             "1536), clock %.2f GHz\n",
+             round, names[mode], us, fl / us * 1e-6, fl / us * 1e-6 / 417.0, cyc / nb / ntiles,
+             ghz / nb);
+      fflush(stdout);
+    }
+  }
+  return 0;
+}
