@@ -8,15 +8,24 @@
 //   mode 1: 8 waves x 64x32, 18 fragment reads (ds_read_b128) per wave and tile
 //   mode 2: 4 waves x 64x64, 24 fragment reads per wave and tile
 //   mode 3: mode 1 with the reads in the tile's first 18 MFMA gaps (gemm_h3m's placement)
+//   modes 4-6: mode 1 plus the LDS-DMA (buffer_load ... lds, 1 KiB per wave
+//   and piece, L2-resident source) of 6 pieces per wave and tile (gemm_h3m's
+//   128 x 128 tile: 48 KiB per k-tile), 4 pieces (a 256 x 128 tile's bytes per
+//   flop: 36 KiB per 128 x 128 equivalent, rounded to 32) and 3 pieces
+//   mode 7: registers (no reads) plus the 6-piece DMA
+//   modes 8-10: modes 4 / 7 / 4 with the pieces of each SIMD's second wave
+//   (waves 4-7) 2 gaps later / 2 gaps later / 14 gaps earlier
 // Prints us per launch, TF-eq and the in-kernel clock (s_memtime / s_memrealtime).
 //   hipcc -O3 --offload-arch=gfx950 tools/mfma_lds_power_bench.hip -o tools/mfma_lds_power_bench
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
 
 #define CHECK(x)                                                                       \
   do {                                                                                 \
@@ -48,12 +57,26 @@ __device__ __forceinline__ void rd_step(bf16x8 (&na)[3][4], bf16x8 (&nb)[3][TB],
 // MFMA M of the tile's 6 * 4 * TB (product-outer: 4 * TB independent MFMAs
 // between dependent ones), accumulators pinned in AGPRs (the compiler's own
 // allocation shuffles them through VGPRs at 4 x 4 blocks)
-template <int TB, bool READ, bool FRONT, int M>
+// DMA piece d goes after MFMA gap 20 + 4 d (gemm_h3m's DG0 / DGS, scaled with TB)
+struct Dma {
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned voff, soff;
+  char* dst;  // this wave's LDS pieces
+};
+template <int TB, bool READ, bool FRONT, int DMA, int DOFF, int M>
 __device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
                                         bf16x8 (&na)[3][4], bf16x8 (&nb)[3][TB],
-                                        f32x4 (&acc)[4][TB], f32x4 (&acs)[4][TB], unsigned lbase) {
+                                        f32x4 (&acc)[4][TB], f32x4 (&acs)[4][TB], unsigned lbase,
+                                        const Dma& dm) {
   constexpr int NMF = 6 * 4 * TB;
   if constexpr (M < NMF) {
+    constexpr int DG0 = 20 * TB / 2 + DOFF, DGS = 4 * TB / 2;
+    if constexpr (M >= DG0 && (M - DG0) % DGS == 0 && (M - DG0) / DGS < DMA) {
+      constexpr int d = (M - DG0) / DGS;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dm.rs, (lds_void*)(dm.dst + d * 1024), 16, dm.voff,
+                                               dm.soff + d * 65536, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     constexpr int q = M / (4 * TB), i = (M / TB) % 4, j = M % TB;
     constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
     if constexpr (READ) rd_step<TB, FRONT, M, 0>(na, nb, lbase);
@@ -63,65 +86,84 @@ __device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
     else
       asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                    : "+a"(acc[i][j]) : "v"(fa[PA[q]][i]), "v"(fb[PB[q]][j]));
-    mm_step<TB, READ, FRONT, M + 1>(fa, fb, na, nb, acc, acs, lbase);
+    mm_step<TB, READ, FRONT, DMA, DOFF, M + 1>(fa, fb, na, nb, acc, acs, lbase, dm);
   }
 }
 
 // TB 16-column B fragments, 4 16-row A fragments per wave; READ: reload every
-// fragment from LDS each tile (else keep the registers)
-template <int TB, bool READ, bool FRONT = false>
+// fragment from LDS each tile (else keep the registers); DMA pieces per wave
+// and tile.  All waves read the same fragment image (bank behaviour is per
+// wave), so the DMA region fits beside it.
+template <int TB, bool READ, bool FRONT = false, int DMA = 0, int STAG = 0>
 __global__ __launch_bounds__(TB == 2 ? 512 : 256, 1) void loop(const bf16x8* __restrict__ src,
+                                                               const char* __restrict__ dsrc,
                                                                int ntiles, float* out,
                                                                unsigned long long* clk) {
   constexpr int NT = TB == 2 ? 512 : 256;
   constexpr int NF = 3 * (4 + TB);  // fragments per wave and tile
-  __shared__ bf16x8 lds[NF * 64 * (NT / 64)];
+  __shared__ bf16x8 lds[NF * 64];
+  __shared__ __attribute__((aligned(16))) char dlds[DMA > 0 ? (NT / 64) * DMA * 1024 : 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   bf16x8 a[3][4], b[3][TB];
-  for (int i = tid; i < NF * NT; i += NT) lds[i] = src[i % (18 * 512)];
+  for (int i = tid; i < NF * 64; i += NT) lds[i] = src[i % (18 * 512)];
   __syncthreads();
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[p][i] = lds[(wave * NF + p * (4 + TB) + i) * 64 + lane];
+    for (int i = 0; i < 4; ++i) a[p][i] = lds[(p * (4 + TB) + i) * 64 + lane];
 #pragma unroll
-    for (int j = 0; j < TB; ++j) b[p][j] = lds[(wave * NF + p * (4 + TB) + 4 + j) * 64 + lane];
+    for (int j = 0; j < TB; ++j) b[p][j] = lds[(p * (4 + TB) + 4 + j) * 64 + lane];
   }
+  // DMA source: 64 KiB per piece index, 3 MiB window shared by all blocks
+  // (L2 / MALL resident like the product's re-read operand tiles)
+  Dma dm;
+  dm.rs = __builtin_amdgcn_make_buffer_rsrc((void*)dsrc, 0, 0x7fffffff, 0x00020000);
+  dm.voff = (unsigned)((wave * 64 + lane) * 16 + (blockIdx.x % 8) * 8192);
+  dm.dst = (char*)dlds + wave * DMA * 1024;
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
   f32x4 acc[4][TB], acs[4][TB];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < TB; ++j) acc[i][j] = acs[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int wslot = (wave * NF) * 64 + lane;
-  // accumulators pinned in AGPRs (the compiler's own allocation shuffles
-  // them through VGPRs at 4 x 4 blocks); product-outer order keeps 4*TB
-  // independent MFMAs between dependent ones
   // READ: double-buffered like the product kernel: tile t+1's fragments are
   // read (hand-issued ds_read_b128, spread evenly between tile t's MFMAs so
   // the 15-deep lgkmcnt never stalls the MFMA chain) and waited for at the
-  // tile's end.  The same slot every tile: the LDS traffic, not the data,
-  // is measured.
-  const unsigned lbase = (unsigned)(size_t)&lds[wslot];  // fragment r at + r KiB
-  auto mm_ld = [&](bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB], bf16x8 (&na)[3][4],
-                   bf16x8 (&nb)[3][TB]) {
-    mm_step<TB, READ, FRONT, 0>(fa, fb, na, nb, acc, acs, lbase);
-    if constexpr (READ) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
+  // tile's end; the tile's DMA pieces may stay in flight one tile.  The same
+  // slot every tile: the LDS traffic, not the data, is measured.
+  const unsigned lbase = (unsigned)(size_t)&lds[lane];  // fragment r at + r KiB
+  // the whole k-loop per placement, chosen by a wave-uniform (scalar) branch
+  // outside it, so each copy keeps its own register assignment
   bf16x8 a2[3][4], b2[3][TB];
-  for (int t = 0; t < ntiles; t += 2) {
-    mm_ld(a, b, a2, b2);
-    __builtin_amdgcn_s_barrier();
-    mm_ld(READ ? a2 : a, READ ? b2 : b, a, b);
-    __builtin_amdgcn_s_barrier();
-    if constexpr (!READ) {
+  auto kloop = [&](auto doff_c) {
+    constexpr int DOFF = decltype(doff_c)::value;
+    auto mm_ld = [&](int t, bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB], bf16x8 (&na)[3][4],
+                     bf16x8 (&nb)[3][TB]) {
+      dm.soff = (unsigned)(t % 48) * 65536u / 4u;
+      mm_step<TB, READ, FRONT, DMA, DOFF, 0>(fa, fb, na, nb, acc, acs, lbase, dm);
+      if constexpr (READ) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (DMA > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA) : "memory");
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+      mm_ld(t, a, b, a2, b2);
+      __builtin_amdgcn_s_barrier();
+      mm_ld(t + 1, READ ? a2 : a, READ ? b2 : b, a, b);
+      __builtin_amdgcn_s_barrier();
+      if constexpr (!READ) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        for (int j = 0; j < TB; ++j) asm volatile("" : "+v"(b[p][j]));
-        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[p][i]));
+        for (int p = 0; p < 3; ++p) {
+          for (int j = 0; j < TB; ++j) asm volatile("" : "+v"(b[p][j]));
+          for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[p][i]));
+        }
       }
     }
-  }
+  };
+  // the SIMD's second wave (waves NT/128 ..) puts its pieces STAG gaps later
+  if (STAG != 0 && __builtin_amdgcn_readfirstlane(wave) >= NT / 128)
+    kloop(std::integral_constant<int, STAG>{});
+  else
+    kloop(std::integral_constant<int, 0>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long r1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
   float sum = 0.f;
   for (int i = 0; i < 4; ++i)
@@ -147,6 +189,10 @@ int main() {
   bf16x8* src;
   float* out;
   unsigned long long* clk;
+  char* dsrc;  // DMA window: 48 piece indices x 64 KiB / 4 apart + 8 KiB x 8 + 512 x 16 B
+  const size_t dbytes = 48 * 16384 + 8 * 8192 + 8 * 1024 * 6 + 4096;
+  CHECK(hipMalloc(&dsrc, dbytes + 6 * 65536));
+  CHECK(hipMemset(dsrc, 0x3c, dbytes + 6 * 65536));
   CHECK(hipMalloc(&src, h.size() * 2));
   CHECK(hipMalloc(&out, nb * 512 * 4));
   CHECK(hipMalloc(&clk, nb * 2 * 8));
@@ -154,19 +200,32 @@ int main() {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  static const char* names[4] = {"8 waves 64x32, registers   ", "8 waves 64x32, 18 reads/tile",
-                                 "4 waves 64x64, 24 reads/tile", "8 waves 64x32, 18 front-read"};
+  static const char* names[11] = {
+      "8 waves 64x32, registers          ", "8 waves 64x32, 18 reads/tile      ",
+      "4 waves 64x64, 24 reads/tile      ", "8 waves 64x32, 18 front-read      ",
+      "8 waves 64x32, 18 reads + 6 DMA   ", "8 waves 64x32, 18 reads + 4 DMA   ",
+      "8 waves 64x32, 18 reads + 3 DMA   ", "8 waves 64x32, registers + 6 DMA  ",
+      "8 w, 18 reads + 6 DMA, stagger 2  ", "8 w, registers + 6 DMA, stagger 2 ",
+      "8 w, 18 reads + 6 DMA, stagger 14 "};
   for (int round = 0; round < 3; ++round) {
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = 0; mode < 11; ++mode) {
       auto launch = [&]() {
-        if (mode == 0)
-          hipLaunchKernelGGL((loop<2, false>), dim3(nb), dim3(512), 0, 0, src, ntiles, out, clk);
-        else if (mode == 1)
-          hipLaunchKernelGGL((loop<2, true>), dim3(nb), dim3(512), 0, 0, src, ntiles, out, clk);
-        else if (mode == 2)
-          hipLaunchKernelGGL((loop<4, true>), dim3(nb), dim3(256), 0, 0, src, ntiles, out, clk);
-        else
-          hipLaunchKernelGGL((loop<2, true, true>), dim3(nb), dim3(512), 0, 0, src, ntiles, out, clk);
+#define L(TB, ...) hipLaunchKernelGGL((loop<TB, __VA_ARGS__>), dim3(nb), dim3(TB == 2 ? 512 : 256), 0, 0, \
+                                      src, dsrc, ntiles, out, clk)
+        switch (mode) {
+          case 0: L(2, false); break;
+          case 1: L(2, true); break;
+          case 2: L(4, true); break;
+          case 3: L(2, true, true); break;
+          case 4: L(2, true, false, 6); break;
+          case 5: L(2, true, false, 4); break;
+          case 6: L(2, true, false, 3); break;
+          case 7: L(2, false, false, 6); break;
+          case 8: L(2, true, false, 6, 2); break;
+          case 9: L(2, false, false, 6, 2); break;
+          default: L(2, true, false, 6, -14); break;
+        }
+#undef L
       };
       for (int i = 0; i < 3; ++i) launch();
       CHECK(hipDeviceSynchronize());
