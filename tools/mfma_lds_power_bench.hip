@@ -15,6 +15,7 @@
 //   mode 7: registers (no reads) plus the 6-piece DMA
 //   modes 8-10: modes 4 / 7 / 4 with the pieces of each SIMD's second wave
 //   (waves 4-7) 2 gaps later / 2 gaps later / 14 gaps earlier
+//   mode 11: mode 4 with global_load_lds instead of buffer_load ... lds
 // Prints us per launch, TF-eq and the in-kernel clock (s_memtime / s_memrealtime).
 //   hipcc -O3 --offload-arch=gfx950 tools/mfma_lds_power_bench.hip -o tools/mfma_lds_power_bench
 #include <hip/hip_runtime.h>
@@ -60,10 +61,11 @@ __device__ __forceinline__ void rd_step(bf16x8 (&na)[3][4], bf16x8 (&nb)[3][TB],
 // DMA piece d goes after MFMA gap 20 + 4 d (gemm_h3m's DG0 / DGS, scaled with TB)
 struct Dma {
   __amdgpu_buffer_rsrc_t rs;
+  const char* g;  // GLOBAL: this lane's source for global_load_lds
   unsigned voff, soff;
   char* dst;  // this wave's LDS pieces
 };
-template <int TB, bool READ, bool FRONT, int DMA, int DOFF, int M>
+template <int TB, bool READ, bool FRONT, int DMA, int DOFF, bool GLOBAL, int M>
 __device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
                                         bf16x8 (&na)[3][4], bf16x8 (&nb)[3][TB],
                                         f32x4 (&acc)[4][TB], f32x4 (&acs)[4][TB], unsigned lbase,
@@ -73,8 +75,12 @@ __device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
     constexpr int DG0 = 20 * TB / 2 + DOFF, DGS = 4 * TB / 2;
     if constexpr (M >= DG0 && (M - DG0) % DGS == 0 && (M - DG0) / DGS < DMA) {
       constexpr int d = (M - DG0) / DGS;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dm.rs, (lds_void*)(dm.dst + d * 1024), 16, dm.voff,
-                                               dm.soff + d * 65536, 0, 0);
+      if constexpr (GLOBAL)
+        __builtin_amdgcn_global_load_lds((const void*)(dm.g + dm.soff + d * 65536),
+                                         (lds_void*)(dm.dst + d * 1024), 16, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dm.rs, (lds_void*)(dm.dst + d * 1024), 16,
+                                                 dm.voff, dm.soff + d * 65536, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     constexpr int q = M / (4 * TB), i = (M / TB) % 4, j = M % TB;
@@ -86,7 +92,7 @@ __device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
     else
       asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                    : "+a"(acc[i][j]) : "v"(fa[PA[q]][i]), "v"(fb[PB[q]][j]));
-    mm_step<TB, READ, FRONT, DMA, DOFF, M + 1>(fa, fb, na, nb, acc, acs, lbase, dm);
+    mm_step<TB, READ, FRONT, DMA, DOFF, GLOBAL, M + 1>(fa, fb, na, nb, acc, acs, lbase, dm);
   }
 }
 
@@ -94,7 +100,7 @@ __device__ __forceinline__ void mm_step(bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB],
 // fragment from LDS each tile (else keep the registers); DMA pieces per wave
 // and tile.  All waves read the same fragment image (bank behaviour is per
 // wave), so the DMA region fits beside it.
-template <int TB, bool READ, bool FRONT = false, int DMA = 0, int STAG = 0>
+template <int TB, bool READ, bool FRONT = false, int DMA = 0, int STAG = 0, bool GLOBAL = false>
 __global__ __launch_bounds__(TB == 2 ? 512 : 256, 1) void loop(const bf16x8* __restrict__ src,
                                                                const char* __restrict__ dsrc,
                                                                int ntiles, float* out,
@@ -120,6 +126,7 @@ __global__ __launch_bounds__(TB == 2 ? 512 : 256, 1) void loop(const bf16x8* __r
   dm.rs = __builtin_amdgcn_make_buffer_rsrc((void*)dsrc, 0, 0x7fffffff, 0x00020000);
   dm.voff = (unsigned)((wave * 64 + lane) * 16 + (blockIdx.x % 8) * 8192);
   dm.dst = (char*)dlds + wave * DMA * 1024;
+  dm.g = dsrc + dm.voff;
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
   f32x4 acc[4][TB], acs[4][TB];
 #pragma unroll
@@ -140,7 +147,7 @@ __global__ __launch_bounds__(TB == 2 ? 512 : 256, 1) void loop(const bf16x8* __r
     auto mm_ld = [&](int t, bf16x8 (&fa)[3][4], bf16x8 (&fb)[3][TB], bf16x8 (&na)[3][4],
                      bf16x8 (&nb)[3][TB]) {
       dm.soff = (unsigned)(t % 48) * 65536u / 4u;
-      mm_step<TB, READ, FRONT, DMA, DOFF, 0>(fa, fb, na, nb, acc, acs, lbase, dm);
+      mm_step<TB, READ, FRONT, DMA, DOFF, GLOBAL, 0>(fa, fb, na, nb, acc, acs, lbase, dm);
       if constexpr (READ) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if constexpr (DMA > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA) : "memory");
     };
@@ -200,15 +207,15 @@ int main() {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  static const char* names[11] = {
+  static const char* names[12] = {
       "8 waves 64x32, registers          ", "8 waves 64x32, 18 reads/tile      ",
       "4 waves 64x64, 24 reads/tile      ", "8 waves 64x32, 18 front-read      ",
       "8 waves 64x32, 18 reads + 6 DMA   ", "8 waves 64x32, 18 reads + 4 DMA   ",
       "8 waves 64x32, 18 reads + 3 DMA   ", "8 waves 64x32, registers + 6 DMA  ",
       "8 w, 18 reads + 6 DMA, stagger 2  ", "8 w, registers + 6 DMA, stagger 2 ",
-      "8 w, 18 reads + 6 DMA, stagger 14 "};
+      "8 w, 18 reads + 6 DMA, stagger 14 ", "8 w, 18 reads + 6 global_load_lds"};
   for (int round = 0; round < 3; ++round) {
-    for (int mode = 0; mode < 11; ++mode) {
+    for (int mode = 0; mode < 12; ++mode) {
       auto launch = [&]() {
 #define L(TB, ...) hipLaunchKernelGGL((loop<TB, __VA_ARGS__>), dim3(nb), dim3(TB == 2 ? 512 : 256), 0, 0, \
                                       src, dsrc, ntiles, out, clk)
@@ -223,7 +230,8 @@ int main() {
           case 7: L(2, false, false, 6); break;
           case 8: L(2, true, false, 6, 2); break;
           case 9: L(2, false, false, 6, 2); break;
-          default: L(2, true, false, 6, -14); break;
+          case 10: L(2, true, false, 6, -14); break;
+          default: L(2, true, false, 6, 0, true); break;
         }
 #undef L
       };
