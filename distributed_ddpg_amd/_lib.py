@@ -12,8 +12,17 @@ import numpy as np
 import torch  # noqa: F401  (must precede the library load; see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# DDPG_LIB_PATH: load an alternative build (tuning experiments only)
-LIB_PATH = os.environ.get("DDPG_LIB_PATH") or os.path.join(_HERE, "libddpg_hip.so")
+_REPO = os.path.dirname(_HERE)
+# DDPG_LIB_PATH: a same-box A/B build for the tools/ scripts only; it must live
+# under tools/ab/ or build_variants/ (the tools' own output), never elsewhere
+_ALT = os.environ.get("DDPG_LIB_PATH")
+if _ALT:
+    _alt = os.path.realpath(_ALT)
+    if not any(_alt.startswith(os.path.join(os.path.realpath(_REPO), d) + os.sep)
+               for d in ("tools", "build_variants")):
+        raise ImportError("DDPG_LIB_PATH=%s: only A/B builds under tools/ or build_variants/ "
+                          "may replace the product library" % _ALT)
+LIB_PATH = _ALT or os.path.join(_HERE, "libddpg_hip.so")
 
 DDPG_OK = 0
 DDPG_EINVAL, DDPG_EHIP, DDPG_ENOMEM, DDPG_ESTATE, DDPG_ECOMM = -1, -2, -3, -4, -5
@@ -115,17 +124,22 @@ PROTOTYPES = [
     ("ddpg_crc32c", _c.c_uint32, [_c.c_uint32, _c.c_void_p, _c.c_size_t]),
 ]
 
+_skipped = []
 for _name, _res, _args in PROTOTYPES:
     try:
         _f = getattr(lib, _name)  # AttributeError here == ABI drift
     except AttributeError:
-        # an older build loaded for a same-box comparison (DDPG_LIB_PATH) may
-        # predate entry points added since; the product library never does
-        if os.environ.get("DDPG_LIB_PATH"):
+        # an older A/B build (DDPG_LIB_PATH) may predate entry points added
+        # since: tolerated only on explicit opt-in, and named
+        if _ALT and os.environ.get("DDPG_LIB_ALLOW_MISSING") == "1":
+            _skipped.append(_name)
             continue
         raise
     _f.restype = _res
     _f.argtypes = _args
+if _skipped:
+    import warnings
+    warnings.warn("%s lacks %s (DDPG_LIB_ALLOW_MISSING=1)" % (LIB_PATH, ", ".join(_skipped)))
 
 if lib.ddpg_abi_version() != ABI_VERSION:
     raise ImportError("libddpg_hip.so ABI version mismatch")

@@ -47,7 +47,7 @@ static void ctx_free(ddpg_ctx* c) {
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->dparams, (void*)c->dpw, (void*)c->dact, (void*)c->d_slots,
                   (void*)c->dmean, (void*)c->dscale, (void*)c->dacc, (void*)c->dstats_all,
-                  (void*)c->xbuf})
+                  (void*)c->xbuf, (void*)c->xrs})
     if (p) (void)hipFree(p);
   for (auto st : c->aux)
     if (st) (void)hipStreamDestroy(st);

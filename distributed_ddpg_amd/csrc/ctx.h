@@ -179,6 +179,7 @@ struct ddpg_ctx {
   float* dstats = nullptr;       // [q_max, loss]
   float* dstats_all = nullptr;   // [world][2] all-gathered stats (world > 1)
   __bf16* xbuf = nullptr;        // bf16 configuration: the exchange's bf16 payload (L.total)
+  float* xrs = nullptr;          // bf16 configuration: this rank's fp32 reduce-scatter slices
   double* dacc = nullptr;        // [qmax_sum, loss_sum, steps]
   double *dmean = nullptr, *dscale = nullptr;
   bool has_scaler = false;
@@ -305,6 +306,7 @@ struct ddpg_ctx {
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
   int cworld = 1;  // ranks in the communicator (1 for a 1-rank or a proxy communicator)
+  int crank = 0;   // this rank in the communicator (0 for a proxy communicator)
   // the step graph captures the collectives too (env DDPG_GRAPH_COMM=0: such
   // steps stay eager); cleared if a capture with RCCL calls fails
   bool comm_graph = true;
@@ -433,7 +435,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda, con
                      float* direct = nullptr);
 TkPart tk_part(const float* X, int ldx, int K, const float* W, int ldw, int w_nk, int N,
                const float* bias, int act, float* out, int ldo);
-int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M);
+int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M,
+                  bool* dw_done = nullptr);
 void gemm_flush(ddpg_ctx* c);
 GemmPlan wgrad_launch(ddpg_ctx* c, const float* A, int lda, const float* B, int ldb, int M, int N,
                       int K, float* slab, int cap, float* direct);

@@ -37,9 +37,13 @@ __global__ void cs_spin_scale_kernel(float* b0, long long n0, float* b1, long lo
   for (long long i = i0; i < n1; i += stride) b1[i] = 2.f * b1[i];
 }
 
-// bf16 configuration's exchange payload: the rank's fp32 gradient rounded
-// to bf16 (one rounding, as the bf16 GEMM operands), summed by RCCL in bf16,
-// widened back into the fp32 gradient buffer for Adam
+// bf16 configuration's exchange ("bf16 with fp32
+// accumulation"): an fp32 reduce-scatter (each rank sums its slice of the
+// ranks' fp32 gradients in fp32), the slice rounded once to bf16, a bf16
+// all-gather, widened back into the fp32 gradient buffer for Adam.  Every
+// rank ends with the same bits (the owner's rounding), the sum carries one
+// bf16 rounding whatever N, and the links move 4 + 2 B per element per
+// (N-1)/N instead of 8 (fp32 all-reduce).
 __global__ void f32_to_bf16_kernel(const float* __restrict__ x, long long n,
                                    __bf16* __restrict__ y) {
   const long long i0 = 4 * ((long long)blockIdx.x * blockDim.x + threadIdx.x);
@@ -109,45 +113,75 @@ void allreduce_on_cs(ddpg_ctx* c, int ev, const char* name, float* b0, size_t n0
                        b1, (long long)n1, c->test_cs_spin);
     HIP_TRY(hipGetLastError());
   }
-  // bf16 configuration: half the bytes on the links
+  // bf16 configuration: fp32 reduce-scatter + bf16 all-gather
   const bool half = c->xbuf != nullptr;
-  __bf16* h0 = half ? c->xbuf : nullptr;
-  __bf16* h1 = half ? c->xbuf + n0 : nullptr;
-  auto conv = [&](bool in) {
-    for (int k = 0; k < 2; ++k) {
-      const size_t n = k ? n1 : n0;
-      if (!n) continue;
-      const int blocks = (int)std::min<size_t>(2048, (n + 1023) / 1024);
-      if (in)
-        hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(blocks), dim3(256), 0, c->cs, k ? b1 : b0,
-                           (long long)n, k ? h1 : h0);
-      else
-        hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(blocks), dim3(256), 0, c->cs, k ? h1 : h0,
-                           (long long)n, k ? b1 : b0);
-      HIP_TRY(hipGetLastError());
-    }
-  };
+  const int N = c->cworld;
+  float* const bs[2] = {b0, b1};
+  const size_t ns[2] = {n0, n1};
+  // per range: m = the largest multiple of N in n (reduce-scattered, chunk
+  // elements per rank), the n - m tail elements all-reduced in fp32
+  size_t m[2], chunk[2];
+  __bf16* h[2] = {nullptr, nullptr};
+  float* rs[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; ++k) {
+    m[k] = ns[k] - ns[k] % N;
+    chunk[k] = m[k] / N;
+  }
+  if (half) {
+    h[0] = c->xbuf;
+    h[1] = c->xbuf + n0;
+    rs[0] = c->xrs;
+    rs[1] = c->xrs + ((chunk[0] + 3) & ~(size_t)3);  // 16-B aligned (float4 reads)
+  }
+  auto blocks = [](size_t n) { return (int)std::min<size_t>(2048, (n + 1023) / 1024); };
   {
     ProfScope ps(c, name, 0,
-                 (double)(n0 + n1) * (half ? 2.0 : 4.0) + (with_stats ? 8.0 * c->cworld : 0.0));
-    if (half) conv(true);
+                 (double)(n0 + n1) * (half ? 3.0 : 4.0) + (with_stats ? 8.0 * c->cworld : 0.0));
     // the group is closed on every path: a call that fails inside it still
     // runs ncclGroupEnd before the error propagates, so the thread's group
     // depth is back to zero for the caller's next (eager) step
     nccl_try(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
-    if (n0)
-      r = half ? ncclAllReduce(h0, h0, n0, ncclBfloat16, ncclSum, c->comm, c->cs)
-               : ncclAllReduce(b0, b0, n0, ncclFloat, ncclSum, c->comm, c->cs);
-    if (r == ncclSuccess && n1)
-      r = half ? ncclAllReduce(h1, h1, n1, ncclBfloat16, ncclSum, c->comm, c->cs)
-               : ncclAllReduce(b1, b1, n1, ncclFloat, ncclSum, c->comm, c->cs);
+    for (int k = 0; k < 2 && r == ncclSuccess; ++k) {
+      if (!ns[k]) continue;
+      if (!half) {
+        r = ncclAllReduce(bs[k], bs[k], ns[k], ncclFloat, ncclSum, c->comm, c->cs);
+        continue;
+      }
+      if (chunk[k])
+        r = ncclReduceScatter(bs[k], rs[k], chunk[k], ncclFloat, ncclSum, c->comm, c->cs);
+      if (r == ncclSuccess && ns[k] > m[k])
+        r = ncclAllReduce(bs[k] + m[k], bs[k] + m[k], ns[k] - m[k], ncclFloat, ncclSum, c->comm,
+                          c->cs);
+    }
     if (r == ncclSuccess && with_stats)
       r = ncclAllGather(c->dstats, c->dstats_all, 2, ncclFloat, c->comm, c->cs);
-    const ncclResult_t re = ncclGroupEnd();
+    ncclResult_t re = ncclGroupEnd();
     nccl_try(r);
     nccl_try(re);
-    if (half) conv(false);
+    if (half && (chunk[0] || chunk[1])) {
+      // this rank's fp32 sums rounded once, into its slot of the gather
+      for (int k = 0; k < 2; ++k)
+        if (chunk[k]) {
+          hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(blocks(chunk[k])), dim3(256), 0, c->cs,
+                             rs[k], (long long)chunk[k], h[k] + (size_t)c->crank * chunk[k]);
+          HIP_TRY(hipGetLastError());
+        }
+      nccl_try(ncclGroupStart());
+      for (int k = 0; k < 2 && r == ncclSuccess; ++k)
+        if (chunk[k])
+          r = ncclAllGather(h[k] + (size_t)c->crank * chunk[k], h[k], chunk[k], ncclBfloat16,
+                            c->comm, c->cs);
+      re = ncclGroupEnd();
+      nccl_try(r);
+      nccl_try(re);
+      for (int k = 0; k < 2; ++k)
+        if (chunk[k]) {
+          hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(blocks(m[k])), dim3(256), 0, c->cs, h[k],
+                             (long long)m[k], bs[k]);
+          HIP_TRY(hipGetLastError());
+        }
+    }
   }
   c->cur = prev;
 }
@@ -192,8 +226,12 @@ static void comm_setup(ddpg_ctx* c, int cworld) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (!c->dstats_all) HIP_TRY(hipMalloc(&c->dstats_all, 2 * (size_t)cworld * sizeof(float)));
   if (!c->cs) HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
-  if (c->cfg.dtype == DDPG_BF16 && !c->xbuf)
+  if (c->cfg.dtype == DDPG_BF16 && !c->xbuf) {
     HIP_TRY(hipMalloc(&c->xbuf, (size_t)c->L.total * sizeof(__bf16)));
+    // the reduce-scatter slices of one call's ranges: at most L.total / cworld
+    // floats (+ alignment); L.total covers every communicator size
+    HIP_TRY(hipMalloc(&c->xrs, ((size_t)c->L.total + 8) * sizeof(float)));
+  }
   for (auto& ev : c->cev)
     if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 }
@@ -223,6 +261,7 @@ int ddpg_comm_init(ddpg_ctx* c, const char* id128, int world, int rank) {
     comm_setup(c, world);
     nccl_try(ncclCommInitRank(&c->comm, world, id, rank));
     c->cworld = world;
+    c->crank = rank;
   });
 }
 
@@ -234,6 +273,7 @@ int ddpg_comm_init_proxy(ddpg_ctx* c) {
     comm_setup(c, 1);
     nccl_try(ncclCommInitRank(&c->comm, 1, id, 0));
     c->cworld = 1;
+    c->crank = 0;
   });
 }
 

@@ -522,7 +522,9 @@ void gemm_flush(ddpg_ctx* c) {
   }
 }
 
-int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M) {
+int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts, int M,
+                  bool* dw_done) {
+  if (dw_done) *dw_done = false;
   if (!c->sw.thin_k || nparts < 1 || nparts > TK_MAXP) return 0;
   TkPart pp[TK_MAXP];
   for (int i = 0; i < nparts; ++i) {
@@ -578,11 +580,15 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
     bwd = bwd && full && !q.bias && q.act == 0 && q.aux && q.colsum && q.ldaux % 4 == 0;
   }
   // a fused weight gradient (TkPart.dw) needs the aux rows (backward or
-  // generic form) and full row tiles
+  // generic form) and full row tiles; a part that cannot carry it runs
+  // unfused (the caller sees *dw_done false and computes it elsewhere)
+  bool dw_all = true;
   for (int i = 0; i < nparts; ++i)
     if (a.p[i].dw && !(!fwd && a.p[i].aux && M % TK_ROWS == 0 && a.p[i].dw_k >= 1 &&
-                       a.p[i].dw_k <= a.p[i].K && a.p[i].K <= 32))
-      return 0;
+                       a.p[i].dw_k <= a.p[i].K && a.p[i].K <= 32)) {
+      a.p[i].dw = nullptr;
+      dw_all = false;
+    }
   char key[96];
   snprintf(key, sizeof key, "thin_k_kernel%s|%s", fwd ? "<FWD>" : bwd ? "<BWD>" : "", name);
   if (c->sw.prof_shapes)
@@ -603,6 +609,7 @@ int thin_k_launch(ddpg_ctx* c, const char* name, const TkPart* parts, int nparts
   else
     hipLaunchKernelGGL(thin_k_kernel<0>, grid, dim3(TK_NT), 0, c->cur, a);
   HIP_TRY(hipGetLastError());
+  if (dw_done) *dw_done = dw_all && dw;
   return mt;
 }
 

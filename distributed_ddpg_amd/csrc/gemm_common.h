@@ -267,7 +267,10 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   float* Wps = smem + PR * VS_LD;        // [BN][PN]
   float* red = Wps + BN * PROJ_MAX;      // [NT]
   float* Xs = red + 2 * GNT;             // [PR][<= 64] narrow rows (nw_*, PR == 128)
-  const int nws = (e.nw_out[1] && n0 >= e.nw_col1) ? 1 : 0;  // narrow set of this tile
+  // narrow set of this tile by its column range: set 0 below nw_col1, set 1
+  // from it (nw_col1 = 0: one set over every column); a null set's tiles
+  // carry no partial
+  const int nws = (e.nw_col1 > 0 && n0 >= e.nw_col1) ? 1 : 0;
   const bool nw = PR == 128 && e.nw_out[nws] != nullptr;
   const int PN = (e.proj_n + 3) & ~3;
   if (e.proj_out) {

@@ -573,11 +573,11 @@ static void critic_train_dev(ddpg_ctx* c, int B, float inv_b, bool fused, int nq
   const bool fa = nw_ok(c, c->dhp, c->ldCH2, whp, c->CH2, B, 2 * c->CH1, c->CH2, c->a, c->ldA,
                         c->A, c->nw_Wa) &&
                   c->CH1 % 128 == 0;
+  // each set owns its half's columns (nw_col1 = CH1 whenever either is
+  // fused), so a state-only fusion never runs set 0 over the action half
   if (fs) nw_set(e, 0, c->s, c->ldS, c->S, c->nw_Ws, c->CH1);
-  if (fa) {
-    nw_set(e, 1, c->a, c->ldA, c->A, c->nw_Wa, c->CH1);
-    e.nw_col1 = c->CH1;
-  }
+  if (fa) nw_set(e, 1, c->a, c->ldA, c->A, c->nw_Wa, c->CH1);
+  if (fs || fa) e.nw_col1 = c->CH1;
   if (fs && fa) e.out = nullptr;
   // one bf16 plane and dWs on the twin GEMM (S > 64, not the skinny kernel):
   // the state half's fp32 values have no reader -- only the action half
@@ -693,8 +693,8 @@ static void actor_train_dev(ddpg_ctx* c, int B, bool fused, bool par = false) {
     tp.dw_k = c->A;
     tp.dw_slab = (long long)c->AH2 * c->A;
   }
-  int mt2 = thin_k_launch(c, "dx", &tp, 1, B);
-  const bool w3_fused = fw3 && mt2 > 0;
+  bool w3_fused = false;
+  int mt2 = thin_k_launch(c, "dx", &tp, 1, B, &w3_fused);
   if (fw3 && !w3_fused)
     pW3 = wgrad_launch(c, c->h2, c->ldAH2, c->dz3, c->ldA, c->AH2, c->A, B, c->slab_W3,
                        c->split_cap_W3, G + L.a[AW3].off);

@@ -364,9 +364,10 @@ def test_small_path_proxy_rank0_of_8(dd, O, clean_env):
 
 def test_proxy_rank0_of_8_c5_bf16_exchange(dd, O, clean_env):
     """The bf16 configuration at C5 dimensions (S = 376, A = 17, 2048 / 2048)
-    exchanges its gradients as bf16 (one rounding of the rank's fp32
-    gradient, RCCL sum in bf16, widened back for Adam: half the bytes of the
-    fp32 exchange).  Rank 0 of 8 at 512 rows per rank through the proxy
+    exchanges its gradients as an fp32 reduce-scatter, one bf16 rounding of
+    each rank's summed slice, a bf16 all-gather, widened back for Adam (6
+    instead of 8 B per element on the links; at N = 1 one rounding of the
+    rank's fp32 gradient).  Rank 0 of 8 at 512 rows per rank through the proxy
     communicator, critic_lr = 0: the critic gradient = the oracle's slice
     mean x 512/4096, the actor gradient = the slice sum, at the stated bf16
     bars (norm-wise and per-tensor max-rel); the exchanged buffers hold
@@ -404,3 +405,107 @@ def test_proxy_rank0_of_8_c5_bf16_exchange(dd, O, clean_env):
             g32 = np.asarray(g, np.float32)
             # exchanged as bf16: the low 16 bits of every fp32 value are zero
             assert np.all((g32.view(np.uint32) & 0xFFFF) == 0), k
+
+
+def _bf16_rne(x):
+    """fp32 -> bf16 (round to nearest even) -> fp32, as the exchange's
+    f32_to_bf16_kernel rounds."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32)
+
+
+def _ring_rs_fp32(parts):
+    """Ring reduce-scatter in fp32: slice j's owner ends the ring, so its sum
+    starts at rank j + 1 and adds the ranks in ring order (each partial sum
+    rounded to fp32)."""
+    n = len(parts)
+    flat = [np.asarray(p, np.float32).ravel() for p in parts]
+    m = flat[0].size - flat[0].size % n
+    ch = m // n
+    out = np.empty(flat[0].size, np.float32)
+    for j in range(n):
+        sl = slice(j * ch, (j + 1) * ch)
+        acc = flat[(j + 1) % n][sl].copy()
+        for k in range(2, n + 1):
+            acc = (acc + flat[(j + k) % n][sl]).astype(np.float32)
+        out[sl] = _bf16_rne(acc)
+    tail = slice(m, flat[0].size)   # all-reduced in fp32
+    acc = flat[0][tail].copy()
+    for k in range(1, n):
+        acc = (acc + flat[k][tail]).astype(np.float32)
+    out[tail] = acc
+    return out, m
+
+
+def _ring_ar_bf16(parts):
+    """The round-5 exchange for comparison: every rank's gradient rounded to
+    bf16, then a bf16 ring sum (each hop's partial rounded to bf16)."""
+    n = len(parts)
+    acc = _bf16_rne(parts[0])
+    for k in range(1, n):
+        acc = _bf16_rne(acc.astype(np.float32) + _bf16_rne(parts[k]))
+    return acc
+
+
+def test_bf16_exchange_fp32_accumulation_8_ranks(dd, O, clean_env):
+    """SURVEY §8(e) step 3, "bf16 with fp32 accumulation", at C5 dimensions
+    and N = 8: the eight ranks' fp32 gradients are computed on the GPU (eight
+    world = 8 contexts, no communicator, 512 rows each of the same global
+    draw of 4096, critic_lr = 0); the exchange the build issues (csrc/dp.hip:
+    fp32 ring reduce-scatter, one bf16 rounding of each slice, bf16
+    all-gather; the n % 8 tail all-reduced in fp32) is emulated on the host
+    with the same per-element arithmetic (the slices follow the concatenated
+    tensors here, the flat buffer's padded ranges in the product).  Its result: every element within one bf16 rounding (2^-8
+    relative) of the fp32 sum, the global-batch oracle gradient at the stated
+    bf16 bars, and no worse than the round-5 bf16 ring sum (per-hop rounding)
+    norm-wise.  The RCCL calls themselves run at N = 1 through the proxy
+    (test_proxy_rank0_of_8_c5_bf16_exchange)."""
+    from test_gpu_configs import BF16_GRAD_MAXREL, BF16_GRAD_NORM_TOL, maxrel
+    from test_gpu_parity import normrel
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale = 376, 17, 2048, 2048, 1.0
+    world, Bg = 8, 4096
+    B = Bg // world
+    p = _noisy_params(O, S, A, H1, H2, seed=63, amp=0.02)
+    rows = _rows(np.random.default_rng(23), 6000, S, A, scale)
+    grads = {"critic": [], "actor": []}
+    for rank in range(world):
+        sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B, rank=rank,
+                                    world=world, dtype="bf16", critic_lr=0.0)
+        rb = ReplayBuffer(8000, 78)
+        rb.add_batch(*rows)
+        FusedLearner(sess, rb, Bg).step()
+        grads["critic"].append(np.concatenate([g.ravel() for g in
+                                               sess.get_params(_lib.CRITIC_GRAD)]))
+        grads["actor"].append(np.concatenate([g.ravel() for g in
+                                              sess.get_params(_lib.ACTOR_GRAD)]))
+        sess.close()
+    idx = np.array(random.Random(78).sample(range(6000), Bg))
+    L = O.Learner(S, A, H1, H2, scale, critic_lr=0.0, dtype=np.float64, params=p,
+                  init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    for net, ref, keys in (("critic", out["critic_grads"], O.CRITIC_KEYS),
+                           ("actor", out["actor_grads"], O.ACTOR_KEYS)):
+        parts = grads[net]
+        new, m = _ring_rs_fp32(parts)
+        old = _ring_ar_bf16(parts)
+        st = np.stack(parts).astype(np.float64)
+        s32, sabs = st.sum(axis=0), np.abs(st).sum(axis=0)
+        assert m > 0.99 * new.size
+        # one bf16 rounding of the sum (2^-9 |x|) + the fp32 ring's partial sums
+        # (<= (N - 1) 2^-24 sum |parts|, what cancellation leaves relative)
+        assert np.all(np.abs(new - s32) <= 2.0 ** -8 * np.abs(s32) + world * 2.0 ** -24 * sabs
+                      + 1e-30), net
+        r = np.concatenate([np.asarray(ref[k], np.float64).ravel() for k in keys])
+        e_new, e_old = normrel(new, r), normrel(old, r)
+        assert e_new <= e_old * 1.0001 + 1e-7, (net, e_new, e_old)
+        off = 0
+        for k in keys:
+            n = np.asarray(ref[k]).size
+            g, rk = new[off:off + n], r[off:off + n]
+            off += n
+            assert normrel(g, rk) < BF16_GRAD_NORM_TOL, (net, k, normrel(g, rk))
+            assert maxrel(g, rk) < BF16_GRAD_MAXREL, (net, k, maxrel(g, rk))
