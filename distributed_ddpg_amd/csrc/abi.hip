@@ -158,6 +158,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.gemm_m16 = !env_is("DDPG_GEMM_M16", "0");
       c->sw.nw_fuse = !env_is("DDPG_NW_FUSE", "0");
       if (const char* v = getenv("DDPG_GEMM256")) c->sw.gemm256 = atoi(v) == 1;
+      if (const char* v = getenv("DDPG_GEMM_HW")) c->sw.gemm_hw = atoi(v) != 0;
       c->sw.xcd = env_is("DDPG_XCD", "0") ? 0 : 1;
       c->sw.xcd_rect = !env_is("DDPG_XCD_RECT", "0");
       c->sw.skinny = !env_is("DDPG_SKINNY", "0");

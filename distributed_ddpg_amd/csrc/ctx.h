@@ -270,6 +270,7 @@ struct ddpg_ctx {
     bool gemm_m16 = true;  // DDPG_GEMM_M16=0: fp32 contexts on the 32x32x16 gemm_h3_kernel instead of gemm_h3m_kernel
     bool nw_fuse = true;   // DDPG_NW_FUSE=0: dW1 / dWs / dWa on the skinny kernel instead of the dX epilogues
     int gemm256 = 0;       // DDPG_GEMM256=1: bf16 split-K weight gradients on gemm_h256.h (opt-in)
+    bool gemm_hw = true;   // DDPG_GEMM_HW=0: bf16 weight gradients on gemm_h16_kernel instead of gemm_hw.h
     int xcd = 1;           // DDPG_XCD=0: no XCD-aware tile order
     bool xcd_rect = true;  // DDPG_XCD_RECT=0: row-major XCD runs only
     bool skinny = true;    // DDPG_SKINNY=0: skinny weight gradients on the GEMMs

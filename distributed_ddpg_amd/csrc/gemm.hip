@@ -9,6 +9,7 @@
 #include "gemm_h.h"
 #include "gemm_h256.h"
 #include "gemm_h3m.h"
+#include "gemm_hw.h"
 #include "thin_k.h"
 #include "skinny.h"
 
@@ -253,6 +254,20 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       }
       h.kps = rup(ceil_div(Kh, std::max(1, splits)), BKh);
       h.splits = ceil_div(Kh, h.kps);
+      // bf16 weight gradients (KR x KR) on gemm_hw_kernel (128 x 64 wave
+      // tiles, 1.2x gemm_h16_kernel): full 256 x 128 tiles, every split a whole
+      // number of its 4-step trips (kps % 128 == 0), the split count at most
+      // the one planned above
+      bool hw = false;
+      if (c->hnp == 1 && AL == L_KR && BL == L_KR && c->sw.gemm_hw && M % 256 == 0 &&
+          N % HG_BN == 0) {
+        for (int sp = h.splits; sp >= 1 && !hw; --sp)
+          if (Kh % sp == 0 && (Kh / sp) % 128 == 0) {
+            hw = true;
+            h.splits = sp;
+            h.kps = Kh / sp;
+          }
+      }
       if (h.splits == 1 && direct) {
         ee.out = direct;
         ee.out_split_stride = 0;
@@ -355,7 +370,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       char shp[48] = "";
       if (c->sw.prof_shapes) snprintf(shp, sizeof shp, " %dx%dx%d/%d", M, N, K, h.splits);
       snprintf(key, sizeof key, "%s<%s,%s,NP=%d>|%s%s%s",
-               h16 ? (AL == L_RK && c->sw.gemm_h3 ? "gemm_h16i_kernel" : "gemm_h16_kernel")
+               hw ? "gemm_hw_kernel"
+               : h16 ? (AL == L_RK && c->sw.gemm_h3 ? "gemm_h16i_kernel" : "gemm_h16_kernel")
                    : (c->hnp == 3 && c->sw.gemm_h3) ? (m16 ? "gemm_h3m_kernel" : "gemm_h3_kernel")
                                                     : "gemm_h_kernel",
                lay[AL], lay[BL], c->hnp, name, a.kpart ? "/kc" : "", shp);
@@ -376,7 +392,10 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
         }
       }
       ProfScope ps(c, key, fl, by);
-      if (h16 && AL == L_RK && c->sw.gemm_h3) {
+      if (hw) {
+        if constexpr (AL == L_KR && BL == L_KR)
+          hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, HG_BN, 4>), grid, dim3(2 * HG_BN), 0, c->cur, a);
+      } else if (h16 && AL == L_RK && c->sw.gemm_h3) {
         // immediate-offset addressing (gemm_h3.h), RK A operands
         if constexpr (AL == L_RK)
           hipLaunchKernelGGL((gemm_h16i_kernel<AL, BL>), grid, dim3(HG_NT), 0, c->cur, a);

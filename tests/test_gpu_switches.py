@@ -43,6 +43,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
                       32 products per MFMA instead of 16, fp32 rounding differs)
   bf16 configuration, different summation order -- the oracle's bf16 bars,
   and the two paths' gradients against each other:
+    DDPG_GEMM_HW=0    the weight gradients on gemm_h16_kernel instead of
+                      gemm_hw_kernel (128 x 64 wave tiles, gemm_hw.h)
     DDPG_GEMM256=1    the split-K weight gradients on the 256 x 256-tile GEMM
                       (gemm_h256.h) instead of gemm_h16_kernel
 """
@@ -62,7 +64,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
-            "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD")
+            "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW")
 
 
 @pytest.fixture(scope="module")
@@ -231,6 +233,7 @@ def test_gemm_h3_switch_bf16_bitwise(dd, O, monkeypatch):
     _clear(monkeypatch)
     monkeypatch.setenv("DDPG_KCOMB", "0")  # gemm_h16_kernel has no in-launch K split
     monkeypatch.setenv("DDPG_NW_FUSE", "0")
+    monkeypatch.setenv("DDPG_GEMM_HW", "0")  # the weight gradients on gemm_h16_kernel both sides
     p, _ = _params(O, "wide")
     ref = _run(dd, O, "wide", p, 2, dtype="bf16", profile=True)
     assert any(k.startswith("gemm_h16i_kernel<RK,KR") for k in ref["keys"]), ref["keys"]
@@ -253,6 +256,7 @@ def test_gemm256_switch_bf16(dd, O, monkeypatch):
     steps meet the oracle's stated bf16 bar (BF16_PARAM_TOL)."""
     from test_gpu_parity import BF16_PARAM_TOL, normrel
     _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_GEMM_HW", "0")  # gemm_h16_kernel is the reference side
     name = "wide"
     p, _ = _params(O, name)
     ref1 = _run(dd, O, name, p, 1, dtype="bf16")
@@ -271,6 +275,37 @@ def test_gemm256_switch_bf16(dd, O, monkeypatch):
         for (net, keys), vals in zip((("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS)),
                                      run["state"][:2]):
             for k, v in zip(keys, vals):
+                assert rel(v, L.state()[net][k].reshape(v.shape)) < BF16_PARAM_TOL, (net, k)
+
+
+def test_gemm_hw_weight_gradients_bf16(dd, O, monkeypatch):
+    """bf16 configuration at the 1024-wide config (B = 256): the weight
+    gradients dWh (2048 x 1024) and dW2 (1024 x 1024) run on gemm_hw_kernel
+    (256 x 128 tiles, 128 x 64 wave tiles, gemm_hw.h) by default and on
+    gemm_h16_kernel with DDPG_GEMM_HW=0.  The same bf16 products with fp32
+    accumulation in another order: the first step's critic gradients agree
+    to 1e-5 norm-wise (the actor's, through the UPDATED critic, to 1e-3), and
+    both runs' parameters after 3 fused steps meet the oracle's bf16 bar."""
+    from test_gpu_parity import BF16_PARAM_TOL, normrel
+    name = "wide"
+    runs = {}
+    for hw in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_GEMM_HW", hw)
+        p, _ = _params(O, name)
+        runs[hw] = (_run(dd, O, name, p, 1, dtype="bf16"),
+                    _run(dd, O, name, p, 3, dtype="bf16", profile=True))
+    keys = {hw: [k for k in r[1]["keys"] if "<KR,KR" in k] for hw, r in runs.items()}
+    assert keys["1"] and all(k.startswith("gemm_hw_kernel<KR,KR,NP=1>") for k in keys["1"]), keys
+    assert keys["0"] and all(k.startswith("gemm_h16_kernel<KR,KR") for k in keys["0"]), keys
+    for bar, x, y in zip((1e-3, 1e-5), runs["0"][0]["state"][8:], runs["1"][0]["state"][8:]):
+        for u, v in zip(x, y):
+            assert normrel(v, u) < bar, normrel(v, u)
+    L, _ = _oracle(O, name, p, runs["1"][1]["rows"], 3)
+    for _, run in runs.values():
+        for (net, keys_), vals in zip((("actor", O.ACTOR_KEYS), ("critic", O.CRITIC_KEYS)),
+                                      run["state"][:2]):
+            for k, v in zip(keys_, vals):
                 assert rel(v, L.state()[net][k].reshape(v.shape)) < BF16_PARAM_TOL, (net, k)
 
 
