@@ -583,14 +583,31 @@ DDPG_DEV void adam_elem(float& p, float& m, float& v, float g, float alpha, floa
   p = __fsub_rn(p, __fdiv_rn(__fmul_rn(m, alpha), __fadd_rn(__fsqrt_rn(v), eps)));
 }
 
+// The element's optimizer state, loaded before its gradient is summed (the
+// loads are independent of the slab sum: issuing them first keeps both round
+// trips in flight instead of one after the other -- the compiler cannot hoist
+// them across the gradient store to a.g, which may alias for all it knows)
 template <class T>
-DDPG_DEV void adam_apply(const AdamArgs& a, long long j, T G, float alpha, float omb1, float omb2);
+struct AdamState {
+  T p, m, v, t;
+};
+template <class T>
+DDPG_DEV AdamState<T> adam_load(const AdamArgs& a, long long j) {
+  AdamState<T> st;
+  st.p = *reinterpret_cast<const T*>(a.p + j);
+  st.m = *reinterpret_cast<const T*>(a.m + j);
+  st.v = *reinterpret_cast<const T*>(a.v + j);
+  if (a.tt) st.t = *reinterpret_cast<const T*>(a.tt + j);
+  return st;
+}
+
+template <class T>
+DDPG_DEV void adam_apply(const AdamArgs& a, long long j, T G, AdamState<T> st, float alpha,
+                         float omb1, float omb2);
 template <>
-DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float4 G, float alpha, float omb1,
-                         float omb2) {
-  float4 P = *reinterpret_cast<float4*>(a.p + j);
-  float4 M = *reinterpret_cast<float4*>(a.m + j);
-  float4 V = *reinterpret_cast<float4*>(a.v + j);
+DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float4 G, AdamState<float4> st,
+                         float alpha, float omb1, float omb2) {
+  float4 P = st.p, M = st.m, V = st.v;
   adam_elem(P.x, M.x, V.x, G.x, alpha, omb1, omb2, a.eps);
   adam_elem(P.y, M.y, V.y, G.y, alpha, omb1, omb2, a.eps);
   adam_elem(P.z, M.z, V.z, G.z, alpha, omb1, omb2, a.eps);
@@ -600,7 +617,7 @@ DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float4 G, float alpha, 
   *reinterpret_cast<float4*>(a.v + j) = V;
   if (a.tw) store_twin4(a.tw + j, a.tps, a.tnp, P);
   if (a.tt) {
-    float4 b = *reinterpret_cast<float4*>(a.tt + j);
+    float4 b = st.t;
     b.x = __fadd_rn(__fmul_rn(P.x, a.tau), __fmul_rn(b.x, a.omt));
     b.y = __fadd_rn(__fmul_rn(P.y, a.tau), __fmul_rn(b.y, a.omt));
     b.z = __fadd_rn(__fmul_rn(P.z, a.tau), __fmul_rn(b.z, a.omt));
@@ -610,16 +627,16 @@ DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float4 G, float alpha, 
   }
 }
 template <>
-DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float G, float alpha, float omb1,
-                         float omb2) {
-  float P = a.p[j], M = a.m[j], V = a.v[j];
+DDPG_DEV void adam_apply(const AdamArgs& a, long long j, float G, AdamState<float> st, float alpha,
+                         float omb1, float omb2) {
+  float P = st.p, M = st.m, V = st.v;
   adam_elem(P, M, V, G, alpha, omb1, omb2, a.eps);
   a.p[j] = P;
   a.m[j] = M;
   a.v[j] = V;
   if (a.tw) store_twin1(a.tw + j, a.tps, a.tnp, P);
   if (a.tt) {
-    const float b = __fadd_rn(__fmul_rn(P, a.tau), __fmul_rn(a.tt[j], a.omt));
+    const float b = __fadd_rn(__fmul_rn(P, a.tau), __fmul_rn(st.t, a.omt));
     a.tt[j] = b;
     if (a.ttw) store_twin1(a.ttw + j, a.tps, a.tnp, b);
   }
@@ -636,17 +653,20 @@ DDPG_DEV void adam_seg(const AdamSeg& g, const AdamArgs& a, int lb, T* part, flo
   const int e = threadIdx.x % EPB, sg = threadIdx.x / EPB;
   for (long long i0 = (long long)lb * EPB; i0 < n; i0 += (long long)g.nblk * EPB) {
     const long long i = i0 + e;
+    const long long j = g.off + i * W;
+    const bool mine = sg == 0 && i < n;  // this thread applies Adam to element i
+    AdamState<T> st{};
+    if (mine) st = adam_load<T>(a, j);
     T acc{};
     if (i < n) acc = slab_partial(src, i, ss, g.nslab, sg, SG);
     if (SG > 1) {
       if (sg > 0) part[(sg - 1) * 256 + e] = acc;
       __syncthreads();
     }
-    if (sg == 0 && i < n) {
+    if (mine) {
       for (int q = 1; q < SG; ++q) acc = rs_add(acc, part[(q - 1) * 256 + e]);
-      const long long j = g.off + i * W;
       if (g.wg) *reinterpret_cast<T*>(a.g + j) = acc;
-      adam_apply(a, j, acc, alpha, omb1, omb2);
+      adam_apply(a, j, acc, st, alpha, omb1, omb2);
     }
     if (SG > 1) __syncthreads();
   }
