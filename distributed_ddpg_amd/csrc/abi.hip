@@ -181,7 +181,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       if (env_is("DDPG_GRAPH_COMM", "0")) c->comm_graph = false;
     }
     if (const char* gv = getenv("DDPG_GRAPH")) c->use_graph = atoi(gv) != 0;
-    if (const char* gv = getenv("DDPG_GRAPH_AUTO")) c->graph_auto = atoi(gv) != 0;
+    if (const char* gv = getenv("DDPG_GRAPH_AUTO")) c->graph_auto = atoi(gv);
     if (const char* pv = getenv("DDPG_PAR")) c->par = atoi(pv) != 0;
     gemm_setup(c);  // split-K caps, small-M buffers, GEMM kernel attributes
     struct Req {

@@ -231,16 +231,19 @@ struct ddpg_ctx {
     hipEvent_t done = nullptr;
   } gslot[2];
   int gcur = 0;
-  // issue policy of the small-batch path (DDPG_GRAPH_AUTO=0: always the
-  // graph): a step that finds the previous one finished (a caller that
-  // synchronises every step, as the reference's worker does) replays the
-  // graph -- the lower latency; a step issued while the previous is still
-  // running (a pipelined caller) is launched eagerly -- the higher throughput
-  // (its 4 launches stream back to back, where a graph launch stalls the queue
-  // at its boundary: C2 +4 % same box; at large B the two measured equal, so
-  // the large path always replays).  Both issue the same kernels in the same
-  // order (bitwise equal results).
-  bool graph_auto = true;
+  // issue policy of the small-batch path (DDPG_GRAPH_AUTO):
+  //   2 (default): always eager -- its 4 launches stream back to back, and a
+  //     synchronous caller (the reference's worker) waits 86-87 us per step
+  //     against 92-94 us for a graph replay (round 6, same box:
+  //     profiles/r6/c2_issue_ab.txt; the graph launch costs more host time
+  //     before the first kernel starts than the first eager launch);
+  //   1: a step that finds the previous one finished replays the graph, a
+  //     step issued while the previous is still running launches eagerly
+  //     (the round-3..5 policy);
+  //   0: always the graph.
+  // Every policy issues the same kernels in the same order (bitwise equal
+  // results); the large path always replays (the two measured equal there).
+  int graph_auto = 2;
   hipEvent_t step_done = nullptr;
   bool use_graph = true;
   bool par = false;  // env DDPG_PAR=1: fork independent branches onto aux streams

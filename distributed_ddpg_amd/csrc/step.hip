@@ -1341,7 +1341,9 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
   // graphs: not profiling (per-kernel events stay eager); a data-parallel
   // step captures its RCCL calls as graph nodes (DDPG_GRAPH_COMM=0: eager)
   bool idle = true;  // the previous step has finished (never-recorded event: success)
-  if (c->graph_auto && small) {
+  if (c->graph_auto == 2 && small) {
+    idle = false;  // small path: always eager
+  } else if (c->graph_auto && small) {
     const hipError_t q = hipEventQuery(c->step_done);
     if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
     idle = q == hipSuccess;

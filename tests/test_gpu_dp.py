@@ -24,7 +24,8 @@ from test_gpu_parity import CONFIGS, GRAD_TOL, _fill, _params, _session, rel
 
 pytestmark = pytest.mark.gpu
 
-ENV = ("DDPG_KCOMB", "DDPG_KCOMB_BLOCKS", "DDPG_GRAPH", "DDPG_GRAPH_COMM", "DDPG_PAR", "DDPG_GEMM_M16",
+ENV = ("DDPG_KCOMB", "DDPG_KCOMB_BLOCKS", "DDPG_GRAPH", "DDPG_GRAPH_COMM", "DDPG_GRAPH_AUTO",
+       "DDPG_PAR", "DDPG_GEMM_M16",
        "DDPG_TEST_CS_SPIN", "DDPG_SMALL")
 
 
@@ -319,8 +320,11 @@ def test_small_path_communicator_matches_no_comm(dd, O, clean_env, graph_comm):
     as two launches around the RCCL sum of its gradient range.  Through a
     1-rank communicator (an identity exchange) three fused steps equal the
     communicator-less step bitwise -- state, per-step stats and running sums
-    -- replayed from a graph holding the RCCL calls or launched eagerly."""
+    -- replayed from a graph holding the RCCL calls or launched eagerly
+    (DDPG_GRAPH_AUTO=1: the synchronised steps replay the graph; the small
+    path's default issues every step eagerly)."""
     S, A, H1, H2, scale = IP
+    clean_env.setenv("DDPG_GRAPH_AUTO", "1")
     p = _noisy_params(O, S, A, H1, H2, seed=60)
     rows = _rows(np.random.default_rng(20), 3000, S, A, scale)
     ref = _ip_run(dd, O, p, rows, 256, 256, steps=3)

@@ -369,7 +369,8 @@ def test_batch_4096_wide_step_properties(dd, O):
 def test_graph_replay_matches_eager(dd, O, monkeypatch, name):
     """The hipGraph-replayed fused step is bit-identical to eager launches
     (all kernels are deterministic: no atomics in any reduction).  Variants:
-    the default issue policy (graph replay when the previous step has
+    the default issue policy (small path: every step eager; large path: graph
+    replay), DDPG_GRAPH_AUTO=1 (graph replay when the previous step has
     finished, eager launches when it is still running: steps without stats
     are not synchronised, so this run mixes both), graph replay only
     (DDPG_GRAPH_AUTO=0) and eager only (DDPG_GRAPH=0)."""
@@ -379,7 +380,7 @@ def test_graph_replay_matches_eager(dd, O, monkeypatch, name):
     S, A, H1, H2, scale, B, _ = CONFIGS[name]
     p, _ = _params(O, name)
     out = []
-    for graph, auto in (("1", "1"), ("1", "0"), ("0", "1")):
+    for graph, auto in (("1", "2"), ("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("DDPG_GRAPH", graph)
         monkeypatch.setenv("DDPG_GRAPH_AUTO", auto)
         sess, actor, critic = _session(dd, O, name, p)
