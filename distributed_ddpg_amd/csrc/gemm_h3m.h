@@ -3,14 +3,16 @@
 //
 // Why the MFMA shape matters here.  gemm_h3_kernel (32x32x16) issues its
 // MFMAs at 95 % of the pipe's cycle budget (1 600 of 1 536 cycles per k-tile,
-// s_memtime stamps, profiles/r5/h3_phase_*.txt) -- and still reaches only
-// 0.45-0.5 of the 417 TF-eq peak, because under this load the chip holds its
-// clock at 1.2-1.3 GHz: the loop is power-bound, not issue-bound.  The same
-// matrix work on the 16x16x32 shape (same cycles per flop) holds a 15-17 %
-// higher clock: a bare MFMA loop with gemm_h3's per-k-tile work and barrier
-// runs 2.05-2.09 GHz vs 1.75-1.78 GHz, 343 vs 300 TF-eq
-// (tools/mfma_power_bench.hip, profiles/r5/mfma_power.txt; MI355X_MICROARCH.md
-// "DVFS give-back" item 7).
+// s_memtime stamps, profiles/r5/h3_phase_*.txt) when launched back to back in
+// isolation, where the chip holds 1.2-1.3 GHz.  The same matrix work on the
+// 16x16x32 shape (same cycles per flop) holds a 15-17 % higher clock: a bare
+// MFMA loop with gemm_h3's per-k-tile work and barrier runs 2.05-2.09 GHz vs
+// 1.75-1.78 GHz, 343 vs 300 TF-eq (tools/mfma_power_bench.hip,
+// profiles/r5/mfma_power.txt; MI355X_MICROARCH.md "DVFS give-back" item 7).
+// Inside the learner step the chip holds >= 1.9 GHz under this kernel
+// (round 6 PMC wave clock, profiles/r6/clock_c3.txt), where it issues MFMAs
+// <= 0.59 of the time and its waves wait on staging / barriers a third of
+// their lifetime (profiles/r6/stall_c3.txt).
 //
 // Tile 128 x 128 x 32 as gemm_h3_kernel: 8 waves (2 along M x 4 along N),
 // wave tile 64 x 32 = 4 x 2 16x16 output blocks, one 32-deep k-step per

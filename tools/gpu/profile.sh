@@ -19,7 +19,7 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
   -- python3 bench.py $ARGS > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err || exit $?
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o run \
   -- python3 bench.py $ARGS > $OUT/bench_write.json 2> $OUT/bench_write.err || exit $?
-timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES --kernel-trace \
+timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace \
   --output-format csv -d $OUT/pmc_mfma -o run -- python3 bench.py $ARGS > $OUT/bench_mfma.json \
   2> $OUT/bench_mfma.err || exit $?
 M=$(dirname $(find $OUT/pmc_mfma -name 'run_counter_collection.csv' | head -1))
