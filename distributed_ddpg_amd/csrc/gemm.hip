@@ -525,16 +525,30 @@ void gemm_flush(ddpg_ctx* c) {
     } else {
       GemmHPack pk;
       double fl = 0, by = 0;
+      // gemm_hw_pack_kernel (two 4-wave blocks per CU) when every part is a
+      // full-tile forward layer (bias, elu; twin and / or fp32 out) of whole
+      // 64-deep steps
+      bool hw = c->sw.gemm_hw;
       for (size_t j = 0; j < n; ++j) {
         pk.p[j] = q[i + j].a;
         fl += q[i + j].flops;
         by += q[i + j].bytes;
+        const GemmHArgs& a = q[i + j].a;
+        const GemmEpi& e = a.e;
+        hw = hw && a.M % 256 == 0 && a.N % HG_BN == 0 && a.kps == a.K && a.K % 64 == 0 &&
+             !a.kpart && e.bias && e.act == 1 && e.post == 0 && !e.colsum && !e.proj_out &&
+             !e.nw_out[0] && !e.nw_out[1] && !e.out_split_stride;
       }
       char key[128];
-      snprintf(key, sizeof key, "gemm_h16i_pack_kernel<RK,KR,NP=1>|%s", strchr(q[i].key, '|') + 1);
+      snprintf(key, sizeof key, "%s<RK,KR,NP=1>|%s",
+               hw ? "gemm_hw_pack_kernel" : "gemm_h16i_pack_kernel", strchr(q[i].key, '|') + 1);
       ProfScope ps(c, key, fl, by);
-      hipLaunchKernelGGL((gemm_h16i_pack_kernel<L_RK, L_KR>), dim3(q[i].grid.x, q[i].grid.y, n),
-                         dim3(HG_NT), 0, c->cur, pk);
+      if (hw)
+        hipLaunchKernelGGL((gemm_hw_pack_kernel<L_RK, L_KR, HG_BN, 2, 64, 1>),
+                           dim3(q[i].grid.x, q[i].grid.y, n), dim3(2 * HG_BN), 0, c->cur, pk);
+      else
+        hipLaunchKernelGGL((gemm_h16i_pack_kernel<L_RK, L_KR>), dim3(q[i].grid.x, q[i].grid.y, n),
+                           dim3(HG_NT), 0, c->cur, pk);
     }
     HIP_TRY(hipGetLastError());
     i += n;

@@ -245,6 +245,8 @@ DDPG_DEV void gemm_epilogue(f32x16 (&acc)[BM / 64][BN / (32 * WGN)], float* smem
   const bool bias = e.bias != nullptr;
   if constexpr (ONLY == 0)
     epi_apply<BM, BN, WGN, false, 0, 0, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
+  else if constexpr (ONLY == 1)
+    epi_apply<BM, BN, WGN, true, 1, 0, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if constexpr (ONLY == 3)
     epi_apply<BM, BN, WGN, false, 0, 1, MF, FULL>(acc, e, M, N, n0, m0, wm, wn, lane);
   else if (!bias && e.act == 0 && e.post == 0)

@@ -39,7 +39,7 @@ DDPG_DEV void glds16(__amdgpu_buffer_rsrc_t r, lds_void* dst, unsigned voff, uns
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
 }
 
-template <int BN, int NS>
+template <int BN, int NS, int PR_ = 0>
 struct HwCfg {
   static constexpr int BM = 256, BK = 32;
   static constexpr int NW = 2 * (BN / 64);  // waves
@@ -53,7 +53,7 @@ struct HwCfg {
   // gemm_epilogue<256, BN, BN / 64, 16, PR>: PR rows x (BN + 4) + projection
   // panel + reduction (+ at PR = 128 the narrow rows of a fused weight
   // gradient); BN = 256 stages 64 rows per pass, as gemm_h256
-  static constexpr int PR = BN == 256 ? 64 : 128;
+  static constexpr int PR = PR_ ? PR_ : (BN == 256 ? 64 : 128);
   static constexpr int EPI_BYTES =
       (PR * (BN + 4) + BN * PROJ_MAX + 2 * GNT + (PR == 128 ? 128 * 64 : 0)) * 4;
   static constexpr int SMEM_BYTES = RING > EPI_BYTES ? RING : EPI_BYTES;
@@ -61,9 +61,14 @@ struct HwCfg {
   static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "whole pieces");
 };
 
-template <int AL, int BL, int BN, int NS>
-__global__ __launch_bounds__(BN * 2, 1) void gemm_hw_kernel(GemmHArgs g) {
-  using C = HwCfg<BN, NS>;
+// PR: epilogue rows per LDS pass (0: 128, or 64 at BN = 256); PR = 64 at
+// NS = 2 fits two blocks per CU (52 KB of epilogue LDS), without the fused
+// narrow weight gradient (it needs PR = 128)
+// ONLY >= 0: compile one element-wise epilogue variant (gemm_epilogue's),
+// which the two-blocks-per-CU form needs to stay within 256 registers
+template <int AL, int BL, int BN, int NS, int PR, int ONLY>
+DDPG_DEV void gemm_hw_body(const GemmHArgs& g, int z) {
+  using C = HwCfg<BN, NS, PR>;
   constexpr int BM = C::BM, BK = C::BK;
   constexpr int WGN = BN / 64;  // waves along N
   constexpr int TA = 8;         // 16-row A fragments per wave (128 rows)
@@ -77,7 +82,7 @@ __global__ __launch_bounds__(BN * 2, 1) void gemm_hw_kernel(GemmHArgs g) {
   const int wm = wave / WGN, wn = wave % WGN;
   int bx, by;
   xcd_tile(bx, by, g.xcd);
-  const int n0 = bx * BN, m0 = by * BM, z = blockIdx.z;
+  const int n0 = bx * BN, m0 = by * BM;
   const int kbeg = z * g.kps;  // split-K: each split's fp32 slab at out + z out_split_stride
   const int nk = g.kps / BK;   // host: kps % (BK NS) == 0, every split full
 
@@ -279,7 +284,24 @@ __global__ __launch_bounds__(BN * 2, 1) void gemm_hw_kernel(GemmHArgs g) {
         for (int tc = 0; tc < 2; ++tc)
 #pragma unroll
           for (int q = 0; q < 4; ++q) out[I][J][4 * (2 * tr + tc) + q] = acc[2 * I + tr][2 * J + tc][q];
-  gemm_epilogue<256, BN, WGN, 16, C::PR, true>(out, smem, ge, tid, n0, m0, z, bx, by);
+  gemm_epilogue<256, BN, WGN, 16, C::PR, true, ONLY>(out, smem, ge, tid, n0, m0, z, bx, by);
+}
+
+template <int AL, int BL, int BN, int NS, int PR = 0, int ONLY = -1>
+__global__ __launch_bounds__(BN * 2, NS == 2 ? 2 : 1) void gemm_hw_kernel(GemmHArgs g) {
+  gemm_hw_body<AL, BL, BN, NS, PR, ONLY>(g, blockIdx.z);
+}
+
+// Up to GH_MAXP independent GEMMs of one grid shape in one launch (part =
+// blockIdx.z, one split each), as gemm_h16i_pack_kernel: the bf16
+// configuration's batch-only first layers (K = S = 376 -> 384).  At NS = 2 /
+// PR = 64 with the forward epilogue only, two 4-wave blocks share a CU, so
+// one block's prologue and epilogue stores run beside the other's k-loop:
+// 1.18x gemm_h16i_pack_kernel's form isolated on the four C5 first layers
+// (tools/hw_bench.hip, profiles/r6/hw_bench_2x.txt).
+template <int AL, int BL, int BN, int NS, int PR = 0, int ONLY = -1>
+__global__ __launch_bounds__(BN * 2, NS == 2 ? 2 : 1) void gemm_hw_pack_kernel(GemmHPack pk) {
+  gemm_hw_body<AL, BL, BN, NS, PR, ONLY>(pk.p[blockIdx.z], 0);
 }
 
 }  // namespace ddpg

@@ -22,7 +22,8 @@ Switches (read at ddpg_create, so each session below sees its own setting):
     DDPG_TK_RPB=3     thin_k blocks walk 3 row tiles each (W panel staged once,
                       next X tile prefetched) instead of the automatic count
     DDPG_GEMM_PACK=0  the bf16 configuration's S > 64 first layers launched one
-                      by one instead of as one gemm_h16i_pack_kernel launch
+                      by one instead of as one gemm_hw_pack_kernel launch
+                      (gemm_h16i_pack_kernel with DDPG_GEMM_HW=0)
     DDPG_TK_FWD=0     thin_k's forward and backward parts on the generic epilogue
                       instead of the forward / backward forms (same arithmetic,
                       flags and bounds folded away)
@@ -196,18 +197,26 @@ def test_tk_fwd_bf16_bitwise(dd, O, monkeypatch):
 
 def test_gemm_pack_bf16_bitwise(dd, O, monkeypatch):
     """bf16 configuration with S = 200 (first layers on the GEMMs): the four
-    batch-only K = S first layers as one gemm_h16i_pack_kernel launch by
-    default, one gemm_h16i_kernel launch each with DDPG_GEMM_PACK=0 -- the same
-    kernel body per tile, bitwise equal after 2 fused steps.  DDPG_KCOMB=0
-    keeps B = 256 on the unsplit plan the pack takes."""
+    batch-only K = S first layers as one gemm_hw_pack_kernel launch by
+    default (two 4-wave 128 x 64-wave-tile blocks per CU, gemm_hw.h), as one
+    gemm_h16i_pack_kernel launch with DDPG_GEMM_HW=0, and one
+    gemm_h16i_kernel launch each with DDPG_GEMM_PACK=0 -- the same 16x16x32
+    MFMAs per output over the same k order and the same epilogue ops: bitwise
+    equal after 2 fused steps.  DDPG_KCOMB=0 keeps B = 256 on the unsplit plan
+    the pack takes."""
     _clear(monkeypatch)
     monkeypatch.setenv("DDPG_KCOMB", "0")
     p, _ = _params(O, "wides")
     ref = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
-    assert any(k.startswith("gemm_h16i_pack_kernel") for k in ref["keys"]), ref["keys"]
+    assert any(k.startswith("gemm_hw_pack_kernel") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_GEMM_HW", "0")
+    got_h16 = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
+    assert any(k.startswith("gemm_h16i_pack_kernel") for k in got_h16["keys"]), got_h16["keys"]
+    monkeypatch.setenv("DDPG_GEMM_HW", "1")
     monkeypatch.setenv("DDPG_GEMM_PACK", "0")
     got = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
-    assert not any(k.startswith("gemm_h16i_pack_kernel") for k in got["keys"]), got["keys"]
+    assert not any("pack_kernel" in k for k in got["keys"]), got["keys"]
+    _bitwise(got_h16, ref)
     _bitwise(got, ref)
 
 

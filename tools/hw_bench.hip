@@ -64,7 +64,7 @@ struct Case {
   int al, bl, M, N, K;
 };
 
-static float *gA, *gB, *gC, *gR, *gCs;
+static float *gA, *gB, *gC, *gR, *gCs, *gBias;
 static __bf16 *hA, *hB, *gTw;
 
 static double check(const float* ref, const float* out, size_t nc) {
@@ -132,6 +132,16 @@ static void run_case(const Case& c) {
     g.e.h_plane_stride = (long long)nc;
     g.e.h_planes = 1;
   }
+  // first-layer cases (K = 384): the forward epilogue (bias, elu, bf16 twin only)
+  const bool l1 = c.K == 384;
+  if (l1) {
+    g.e.bias = gBias;
+    g.e.act = 1;
+    g.e.out = nullptr;
+    g.e.outh = gTw;
+    g.e.h_plane_stride = (long long)nc;
+    g.e.h_planes = 1;
+  }
   auto fprod = [&] {
     dim3 grid((c.N + 127) / 128, (c.M + 255) / 256, 1);
     if constexpr (AL == L_RK)
@@ -143,35 +153,39 @@ static void run_case(const Case& c) {
     hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 4>), dim3(c.N / 128, c.M / 256, 1),
                        dim3(HwCfg<128, 4>::NT), 0, 0, g);
   };
-  // gemm_h256_kernel MODE 2 (any epilogue, one split) where N % 256 == 0
+  // gemm_hw_kernel at NS = 2, PR = 64: two blocks per CU (one epilogue
+  // variant: the forward one for l1 cases, plain otherwise)
   auto f256 = [&] {
-    if (c.N % 256 == 0)
-      hipLaunchKernelGGL((gemm_h256_kernel<AL, BL, 2>), dim3(c.N / 256, c.M / 256, 1),
-                         dim3(H2_NT), 0, 0, g);
+    if (l1)
+      hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 2, 64, 1>), dim3(c.N / 128, c.M / 256, 1),
+                         dim3(256), 0, 0, g);
+    else if (!epi)
+      hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 2, 64, 0>), dim3(c.N / 128, c.M / 256, 1),
+                         dim3(256), 0, 0, g);
   };
   const double flop = 2.0 * c.M * c.N * (double)c.K;
   for (int rep = 0; rep < 2; ++rep) {
     float us[3];
     double err[3];
-    const char* nm[3] = {"prod", "hw128", "h256"};
+    const char* nm[3] = {"prod", "hw128", "hw2x"};
     for (int v = 0; v < 3; ++v) {
       CHECK(hipMemset(gC, 0, nc * 4));
       us[v] = v == 0 ? time_it(fprod, 10) : v == 1 ? time_it(f128, 10) : time_it(f256, 10);
       CHECK(hipMemcpy(out.data(), gC, nc * 4, hipMemcpyDeviceToHost));
-      err[v] = epi ? -1.0 : check(ref.data(), out.data(), nc);
+      err[v] = (epi || l1) ? -1.0 : check(ref.data(), out.data(), nc);
     }
     printf("%-16s M=%d N=%d K=%d %s", c.name, c.M, c.N, c.K, epi ? "EPI" : "   ");
     for (int v = 0; v < 3; ++v)
       printf(" | %s %7.2f us %6.1f TF err %.1e", nm[v], us[v], flop / (us[v] * 1e-6) / 1e12,
              err[v]);
-    printf(" | hw128 %.2fx h256 %.2fx\n", us[0] / us[1], us[0] / us[2]);
+    printf(" | hw128 %.2fx hw2x %.2fx\n", us[0] / us[1], us[0] / us[2]);
     fflush(stdout);
   }
 }
 
 int main(int argc, char** argv) {
   const char* only = argc > 1 ? argv[1] : nullptr;
-  const size_t maxe = (size_t)4096 * 4096;
+  const size_t maxe = (size_t)16384 * 2048;
   CHECK(hipMalloc(&gA, maxe * 4));
   CHECK(hipMalloc(&gB, maxe * 4));
   CHECK(hipMalloc(&gC, maxe * 4));
@@ -180,7 +194,10 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&hB, maxe * 2));
   CHECK(hipMalloc(&gTw, maxe * 2));
   CHECK(hipMalloc(&gCs, 64 * 4096 * 4));
+  CHECK(hipMalloc(&gBias, 4096 * 4));
+  CHECK(hipMemset(gBias, 0, 4096 * 4));
   const Case cases[] = {
+      {"c5 l1x4 <RK,KR>", L_RK, L_KR, 16384, 2048, 384},
       {"c5 fwd <RK,KR>", L_RK, L_KR, 4096, 2048, 2048},
       {"c5 fwd <RK,KR>", L_RK, L_KR, 4096, 2048, 4096},
       {"c5 dx <RK,RK>", L_RK, L_RK, 4096, 4096, 2048},
