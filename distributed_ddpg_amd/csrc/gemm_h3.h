@@ -333,7 +333,9 @@ namespace ddpg {
 // k-tile advance in the scalar soffset.  RK A operands (forward, dX).  Same
 // schedule and MFMA order: bitwise equal to gemm_h16_kernel
 // (DDPG_GEMM_H3=0 selects it).
-template <int AL, int BL>
+// SPR = 1: the fragment reads of step ks+1 go one read group per MFMA gap of
+// step ks instead of as one burst ahead of its MFMAs (schedule knob)
+template <int AL, int BL, int SPR = 0>
 DDPG_DEV void gemm_h16i_body(const GemmHArgs& g, int z) {
   static_assert(AL == L_RK, "RK A operand");
   constexpr int NP = 1, BM = 256, BK = 64;
@@ -443,6 +445,23 @@ DDPG_DEV void gemm_h16i_body(const GemmHArgs& g, int z) {
       av[0][I] = b128_read_off<I * 16 * (2 * BK)>(a);
     });
   };
+  // one read group of read(): B fragment R (R < TB), else A fragment R - TB
+  auto read_group = [&](unsigned so, auto ks_c, auto r_c, bf16x8 (&av)[NP][TA],
+                        bf16x8 (&bv)[NP][TB]) {
+    constexpr int KSR = decltype(ks_c)::value, R = decltype(r_c)::value;
+    if constexpr (R < TB) {
+      if constexpr (BL == L_RK) {
+        bv[0][R] = b128_read_off<R * 16 * (2 * BK)>(bbase[KSR] + so);
+      } else {
+        constexpr int OFF = KSR * 32 * 256;
+        bv[0][R] = __builtin_shufflevector(tr_read_off<OFF>(bbase[2 * R] + so),
+                                           tr_read_off<OFF>(bbase[2 * R + 1] + so), 0, 1, 2, 3,
+                                           4, 5, 6, 7);
+      }
+    } else {
+      av[0][R - TB] = b128_read_off<(R - TB) * 16 * (2 * BK)>(abase[KSR] + so);
+    }
+  };
   auto mfma_all = [&](bf16x8 (&av)[NP][TA], bf16x8 (&bv)[NP][TB]) {
 #pragma unroll
     for (int i = 0; i < TA; ++i)
@@ -465,21 +484,37 @@ DDPG_DEV void gemm_h16i_body(const GemmHArgs& g, int z) {
       constexpr int ks = decltype(ks_c)::value;
       constexpr int cs = ks & 1, ns = (ks + 1) & 1;
       hg_wait16<NP, TA, TB>(fa[cs], fb[cs]);
-      if constexpr (ks + 1 < KS) {
-        read(so, std::integral_constant<int, ks + 1>{}, fa[ns], fb[ns]);
-      } else if constexpr (NEXT) {
+      if constexpr (ks + 1 == KS && NEXT) {
         if constexpr (G2)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::G) : "memory");
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        read((unsigned)((slot + 1) % HG_STAGES) * C::STAGE, std::integral_constant<int, 0>{},
-             fa[ns], fb[ns]);
       }
+      constexpr bool RD = ks + 1 < KS || NEXT;  // this step reads the next one's fragments
+      const unsigned rso =
+          ks + 1 < KS ? so : (unsigned)((slot + 1) % HG_STAGES) * C::STAGE;
+      constexpr int RKS = ks + 1 < KS ? ks + 1 : 0;
+      if constexpr (!SPR && RD) read(rso, std::integral_constant<int, RKS>{}, fa[ns], fb[ns]);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_all(fa[cs], fb[cs]);
-      if constexpr (ks + 1 == KS && STAGE3) {
+      if constexpr (SPR && RD) {
+        // read group r (B fragment r < TB, then A fragment r - TB) after MFMA r
+        static_for<TA * TB>([&](auto q_c) {
+          constexpr int q = decltype(q_c)::value, i = q / TB, j = q % TB;
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cs][0][i], fb[cs][0][j],
+                                                              acc[i][j], 0, 0, 0);
+          if constexpr (q < TA + TB) read_group(rso, std::integral_constant<int, RKS>{},
+                                                std::integral_constant<int, q>{}, fa[ns], fb[ns]);
+          // the tile-(t+3) LDS-DMA in the gaps after the reads
+          if constexpr (ks + 1 == KS && STAGE3 && q >= TA + TB && q - (TA + TB) < C::G)
+            piece(t + 3, slot, q - (TA + TB));
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      } else {
+        mfma_all(fa[cs], fb[cs]);
+      }
+      if constexpr (ks + 1 == KS && STAGE3 && !(SPR && RD)) {
         stage(t + 3, slot);
         constexpr int NG = C::G, MPG = NM / NG > 0 ? NM / NG : 1;
         static_for<NG>([&](auto) {

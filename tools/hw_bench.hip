@@ -18,6 +18,12 @@
 
 using namespace ddpg;
 
+// gemm_h16i_kernel with the spread-read schedule (SPR = 1)
+template <int AL, int BL>
+__global__ __launch_bounds__(HG_NT, 1) void h16i_spr_kernel(GemmHArgs g) {
+  gemm_h16i_body<AL, BL, 1>(g, blockIdx.z);
+}
+
 #define CHECK(x)                                                                    \
   do {                                                                              \
     hipError_t e_ = (x);                                                            \
@@ -153,21 +159,17 @@ static void run_case(const Case& c) {
     hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 4>), dim3(c.N / 128, c.M / 256, 1),
                        dim3(HwCfg<128, 4>::NT), 0, 0, g);
   };
-  // gemm_hw_kernel at NS = 2, PR = 64: two blocks per CU (one epilogue
-  // variant: the forward one for l1 cases, plain otherwise)
+  // variant 3: gemm_h16i_kernel with spread fragment reads (RK A only)
   auto f256 = [&] {
-    if (l1)
-      hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 2, 64, 1>), dim3(c.N / 128, c.M / 256, 1),
-                         dim3(256), 0, 0, g);
-    else if (!epi)
-      hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 2, 64, 0>), dim3(c.N / 128, c.M / 256, 1),
-                         dim3(256), 0, 0, g);
+    if constexpr (AL == L_RK)
+      hipLaunchKernelGGL((h16i_spr_kernel<AL, BL>), dim3((c.N + 127) / 128, (c.M + 255) / 256, 1),
+                         dim3(HG_NT), 0, 0, g);
   };
   const double flop = 2.0 * c.M * c.N * (double)c.K;
   for (int rep = 0; rep < 2; ++rep) {
     float us[3];
     double err[3];
-    const char* nm[3] = {"prod", "hw128", "hw2x"};
+    const char* nm[3] = {"prod", "hw128", "spr"};
     for (int v = 0; v < 3; ++v) {
       CHECK(hipMemset(gC, 0, nc * 4));
       us[v] = v == 0 ? time_it(fprod, 10) : v == 1 ? time_it(f128, 10) : time_it(f256, 10);
@@ -178,7 +180,7 @@ static void run_case(const Case& c) {
     for (int v = 0; v < 3; ++v)
       printf(" | %s %7.2f us %6.1f TF err %.1e", nm[v], us[v], flop / (us[v] * 1e-6) / 1e12,
              err[v]);
-    printf(" | hw128 %.2fx hw2x %.2fx\n", us[0] / us[1], us[0] / us[2]);
+    printf(" | hw128 %.2fx spr %.2fx\n", us[0] / us[1], us[0] / us[2]);
     fflush(stdout);
   }
 }
