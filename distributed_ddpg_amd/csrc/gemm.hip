@@ -258,6 +258,8 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       // tiles, 1.2x gemm_h16_kernel): full 256 x 128 tiles, every split a whole
       // number of its 4-step trips (kps % 128 == 0), the split count at most
       // the one planned above
+      // (full tiles only: the partial-M dWs / dW1, 376 x 2048, measured 1.02x
+      // isolated and no better in the step, profiles/r6/hw_bench_wgrad_partial.txt)
       bool hw = false;
       if (c->hnp == 1 && AL == L_KR && BL == L_KR && c->sw.gemm_hw && M % 256 == 0 &&
           N % HG_BN == 0) {

@@ -66,7 +66,9 @@ struct HwCfg {
 // narrow weight gradient (it needs PR = 128)
 // ONLY >= 0: compile one element-wise epilogue variant (gemm_epilogue's),
 // which the two-blocks-per-CU form needs to stay within 256 registers
-template <int AL, int BL, int BN, int NS, int PR, int ONLY>
+// FULL = false: M need not be a multiple of 256 (rows past M are read
+// clamped and never stored: the epilogue's bounds checks)
+template <int AL, int BL, int BN, int NS, int PR, int ONLY, bool FULL>
 DDPG_DEV void gemm_hw_body(const GemmHArgs& g, int z) {
   using C = HwCfg<BN, NS, PR>;
   constexpr int BM = C::BM, BK = C::BK;
@@ -284,12 +286,12 @@ DDPG_DEV void gemm_hw_body(const GemmHArgs& g, int z) {
         for (int tc = 0; tc < 2; ++tc)
 #pragma unroll
           for (int q = 0; q < 4; ++q) out[I][J][4 * (2 * tr + tc) + q] = acc[2 * I + tr][2 * J + tc][q];
-  gemm_epilogue<256, BN, WGN, 16, C::PR, true, ONLY>(out, smem, ge, tid, n0, m0, z, bx, by);
+  gemm_epilogue<256, BN, WGN, 16, C::PR, FULL, ONLY>(out, smem, ge, tid, n0, m0, z, bx, by);
 }
 
-template <int AL, int BL, int BN, int NS, int PR = 0, int ONLY = -1>
+template <int AL, int BL, int BN, int NS, int PR = 0, int ONLY = -1, bool FULL = true>
 __global__ __launch_bounds__(BN * 2, NS == 2 ? 2 : 1) void gemm_hw_kernel(GemmHArgs g) {
-  gemm_hw_body<AL, BL, BN, NS, PR, ONLY>(g, blockIdx.z);
+  gemm_hw_body<AL, BL, BN, NS, PR, ONLY, FULL>(g, blockIdx.z);
 }
 
 // Up to GH_MAXP independent GEMMs of one grid shape in one launch (part =
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(BN * 2, NS == 2 ? 2 : 1) void gemm_hw_kernel(GemmHA
 // (tools/hw_bench.hip, profiles/r6/hw_bench_2x.txt).
 template <int AL, int BL, int BN, int NS, int PR = 0, int ONLY = -1>
 __global__ __launch_bounds__(BN * 2, NS == 2 ? 2 : 1) void gemm_hw_pack_kernel(GemmHPack pk) {
-  gemm_hw_body<AL, BL, BN, NS, PR, ONLY>(pk.p[blockIdx.z], 0);
+  gemm_hw_body<AL, BL, BN, NS, PR, ONLY, true>(pk.p[blockIdx.z], 0);
 }
 
 }  // namespace ddpg

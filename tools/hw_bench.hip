@@ -156,7 +156,7 @@ static void run_case(const Case& c) {
       hipLaunchKernelGGL((gemm_h16_kernel<AL, BL, 1, 256, 64>), grid, dim3(HG_NT), 0, 0, g);
   };
   auto f128 = [&] {
-    hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 4>), dim3(c.N / 128, c.M / 256, 1),
+    hipLaunchKernelGGL((gemm_hw_kernel<AL, BL, 128, 4, 0, -1, false>), dim3(c.N / 128, (c.M + 255) / 256, 1),
                        dim3(HwCfg<128, 4>::NT), 0, 0, g);
   };
   // variant 3: gemm_h16i_kernel with spread fragment reads (RK A only)
@@ -205,6 +205,7 @@ int main(int argc, char** argv) {
       {"c5 dx <RK,RK>", L_RK, L_RK, 4096, 4096, 2048},
       {"c5 dx <RK,RK>", L_RK, L_RK, 4096, 2048, 2048},
       {"c5 wgrad <KR,KR>", L_KR, L_KR, 4096, 2048, 4096},
+      {"c5 wgrad dWs <KR,KR>", L_KR, L_KR, 376, 2048, 512},
   };
   for (const Case& c : cases) {
     char full[96];
