@@ -11,20 +11,24 @@
 //              loss / dQ -> critic head + dX backward; saves the activations
 //              and output gradients the critic weight gradients need.  WG 0
 //              computes the critic Adam step size from the beta powers and
-//              advances them (TF AdamOptimizer._finish).
+//              advances them (TF AdamOptimizer._finish).  A second set of
+//              workgroups, on CUs of their own, runs the online actor's
+//              forward on the same rows (its parameters are not updated
+//              before phase 3) and saves h1, h2, o.
 //   sb_wgrad_adam(critic): every critic weight gradient dW = X^T . dY over
 //              the whole batch (one ordered fp32 sum over b per element),
 //              TF ApplyAdam, soft update of the critic target, and the
 //              transposed shadow of Wh used by the dX layers.
-//   sb_phase3  (row-parallel): online actor fwd -> updated-critic fwd at
-//              (s, mu) -> dQ/da -> actor backward; saves what the actor
-//              weight gradients need.  WG 0 computes the actor step size.
+//   sb_phase3  (row-parallel): the saved actor forward -> updated-critic
+//              fwd at (s, mu) -> dQ/da -> actor backward; saves what the
+//              actor weight gradients need.  WG 0 computes the actor step
+//              size.
 //   sb_wgrad_adam(actor) (+ shadow of W2).
 //
 // Inside a phase, independent layers run side by side on disjoint thread
 // groups (e.g. the target actor's first layer, both critics' state branches
 // and the online critic's action branch are one level), so the dependent
-// chain is 8 levels per phase.  Each dense layer is a skinny [SB_R x K] .
+// chain is 8 levels in phase 1 and 5 in phase 3.  Each dense layer is a skinny [SB_R x K] .
 // [K x N] product: the weights are read once per WG straight into VGPRs (the
 // GEMV rule: no LDS round trip), each thread owning one 4-column group of one
 // k-slice, all of a batch's loads issued before the first FMA, then an
@@ -310,16 +314,18 @@ SB_FN void sb_thin_epi(const SbOp& o, int t, int nt, const lds_f* red) {
   }
 }
 
-// One level of NOPS independent layers on NOPS equal wave-aligned thread
-// groups, each with its own slice of red and of the bias area (the bias and
-// pw vectors are loaded before the weights, so their round trip hides behind
-// the weights', and parked in LDS for the epilogue).  Ends with a barrier.
+// One level of NOPS independent layers on NG >= NOPS equal wave-aligned thread
+// groups (groups past NOPS idle), each with its own slice of red and of the
+// bias area (the bias and pw vectors are loaded before the weights, so their
+// round trip hides behind the weights', and parked in LDS for the epilogue).
+// Ends with a barrier.
 constexpr int SB_BIAS = 2048;  // LDS floats for biases (+ as many for pw)
-template <int NOPS>
+template <int NOPS, int NG = NOPS>
 SB_FN void sb_level(const SbOp (&ops)[NOPS], const bool (&thin)[NOPS], lds_f* red) {
-  constexpr int nt = SB_NT / NOPS;
-  constexpr int rs = SB_RED / NOPS;
-  constexpr int bs = SB_BIAS / NOPS;
+  static_assert(NG >= NOPS, "one thread group per layer");
+  constexpr int nt = SB_NT / NG;
+  constexpr int rs = SB_RED / NG;
+  constexpr int bs = SB_BIAS / NG;
   lds_f* bias = red + SB_RED;
   const int grp = threadIdx.x / nt, t = threadIdx.x - grp * nt;
 #pragma unroll
@@ -388,13 +394,65 @@ DDPG_DEV void sb_save(float* __restrict__ save, int Bp, int cols, const lds_f* s
     *reinterpret_cast<f32x4*>(save + (size_t)k * Bp + r0) = s4[k];
 }
 
+// Phase 1's actor-forward workgroups: the online actor's forward on the same
+// rows (networks.py:51-63, ddpg.py:106's actor.predict(s)).  The actor's
+// parameters do not change until its own Adam step, so this runs beside the
+// critic chain on CUs of its own, and phase 3 (after the critic update) reads
+// h1, h2 and o back instead of recomputing them on its critical path.  Same
+// level shapes as phase 3 used, so the values are the ones it computed.
+DDPG_DEV void sb_actor_rows(const SbArgs& g, int r0, int valid, lds_f* red) {
+  const int tid = threadIdx.x;
+  lds_f* xs = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
+  lds_f* o = xs + 4 * g.LX;
+  lds_f* h1 = o + 4 * g.LX;  // [LW][4]
+  lds_f* h2 = h1 + 4 * g.LW;
+  const glb_f* P = GLB(g.theta);
+  for (int idx = tid; idx < 4 * g.LX; idx += SB_NT) {  // as phase 1's critic gather
+    const int k = idx >> 2, r = idx & 3;
+    float x = 0.f;
+    if (r < valid && k < g.S) {
+      const size_t e = (size_t)g.slots[r0 + r] * g.S + k;
+      const double xd = g.rsd ? g.rsd[e] : (double)g.rs[e];
+      x = g.mean ? (float)((xd - g.mean[k]) / g.sdev[k]) : (float)xd;
+    }
+    xs[idx] = x;
+  }
+  __syncthreads();
+  {  // L1 on half the threads: phase 3's former two-group level (its k-slices)
+    const SbOp ops[1] = {sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1)};
+    const bool th[1] = {false};
+    sb_level<1, 2>(ops, th, red);
+  }
+  sb_dense1(sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2), red);
+  sb_thin1(sb_op(h2, g.AH2, P + g.aW3, g.A, g.A, nullptr, SB_NONE, o), false, true, red);
+  sb_save(g.sv.h1, g.sv.Bp, g.AH1, h1, r0);
+  sb_save(g.sv.h2, g.sv.Bp, g.AH2, h2, r0);
+  sb_save(g.sv.o, g.sv.Bp, g.A, o, r0);
+}
+
+// Phase-1 roles: with XCD packing (xstride > 1) block b works as role b %
+// xstride (0: critic rows, 1: actor rows; the rest exit at once), so each
+// role's workgroups share one XCD's L2; otherwise blocks [0, G) are the
+// critic rows and [G, 2G) the actor rows.
 __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x;
-  if (blockIdx.x % g.xstride) return;
-  const int wg = blockIdx.x / g.xstride;
+  const int G = (g.B + SB_R - 1) / SB_R;
+  int wg, role;
+  if (g.xstride > 1) {
+    role = blockIdx.x % g.xstride;
+    wg = blockIdx.x / g.xstride;
+  } else {
+    role = blockIdx.x / G;
+    wg = blockIdx.x - role * G;
+  }
+  if (role > 1 || wg >= G) return;
   const int r0 = wg * SB_R;
   const int valid = min(SB_R, g.B - r0);
+  if (role == 1) {
+    sb_actor_rows(g, r0, valid, LDS(sm));
+    return;
+  }
   const int LX = g.LX, LW = g.LW;
   lds_f* red = LDS(sm);
   lds_f* xs = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
@@ -542,30 +600,38 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   SB_STAMP(32);
 
   if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw, g.alpha, g.lr_a, g.b1, g.b2);
-  for (int idx = tid; idx < 4 * LX; idx += SB_NT) {  // phase 1 saved the (scaled) rows
-    const int k = idx >> 2, r = idx & 3;
-    xs[idx] = (r < valid && k < g.S) ? g.sv.xs[(size_t)k * g.sv.Bp + r0 + r] : 0.f;
+  // phase 1 saved the (scaled) rows and the actor's forward on them
+  // (networks.py:51-63): h1, h2, o; mu = scale o (ddpg.py:106)
+  {
+    const int Bp = g.sv.Bp;
+    auto ld = [&](lds_f* dst, const float* src, int cols, int ld_cols) {
+      for (int idx = tid; idx < 4 * ld_cols; idx += SB_NT) {
+        const int k = idx >> 2, r = idx & 3;
+        dst[idx] = (r < valid && k < cols) ? src[(size_t)k * Bp + r0 + r] : 0.f;
+      }
+    };
+    ld(xs, g.sv.xs, g.S, LX);
+    ld(h1, g.sv.h1, g.AH1, g.AH1);
+    ld(h2, g.sv.h2, g.AH2, g.AH2);
+    for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
+      const int k = idx >> 2, r = idx & 3;
+      const float v = (r < valid && k < g.A) ? g.sv.o[(size_t)k * Bp + r0 + r] : 0.f;
+      o[idx] = v;
+      mu[idx] = __fmul_rn(v, g.scale);
+    }
   }
   __syncthreads();
   SB_STAMP(33);
-  {  // L1: actor h1 | critic state branch
-    const SbOp ops[2] = {sb_op(xs, g.S, P + g.aW1, g.AH1, g.AH1, P + g.ab1, SB_ELU, h1),
-                         sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat)};
+  {  // L1: critic state branch at s | action branch at mu (the updated critic)
+    const SbOp ops[2] = {
+        sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat),
+        sb_op(mu, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, cat + 4 * g.CH1)};
     const bool th[2] = {false, false};
     sb_level<2>(ops, th, red);
   }
-  SB_STAMP(34);
-  // L2: h2; L3: o = tanh(h2 W3), mu = scale o   (networks.py:51-63, ddpg.py:106)
-  sb_dense1(sb_op(h1, g.AH1, P + g.aW2, g.AH2, g.AH2, P + g.ab2, SB_ELU, h2), red);
-  SB_STAMP(35);
-  sb_thin1(sb_op(h2, g.AH2, P + g.aW3, g.A, g.A, nullptr, SB_NONE, o), false, true, red);
-  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) mu[idx] = __fmul_rn(o[idx], g.scale);
-  __syncthreads();
-  SB_STAMP(36);
-  // L4: action branch at mu; L5: dhp2 = Wo * elu'(h')  (updated critic, grad_ys = 1,
-  // networks.py:143); L6: dca = dhp2 . Wh[CH1:]^T * elu'(ca), in place over ca
-  sb_dense1(sb_op(mu, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU, cat + 4 * g.CH1), red);
   SB_STAMP(37);
+  // L5: dhp2 = Wo * elu'(h')  (updated critic, grad_ys = 1, networks.py:143);
+  // L6: dca = dhp2 . Wh[CH1:]^T * elu'(ca), in place over ca
   sb_dense1(sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_POST2, dh, nullptr,
                   P + g.cWo),
             red);
@@ -596,8 +662,6 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
   // L8: dz1 = dz2 . W2^T * elu'(h1) -> cat
   sb_dense1(sb_op(dh, g.AH2, GLB(g.w2T), g.AH1, g.AH1, nullptr, SB_AUX, cat, h1), red);
   SB_STAMP(41);
-  sb_save(g.sv.h1, g.sv.Bp, g.AH1, h1, r0);
-  sb_save(g.sv.h2, g.sv.Bp, g.AH2, h2, r0);
   sb_save(g.sv.dz1, g.sv.Bp, g.AH1, cat, r0);
   sb_save(g.sv.dz2, g.sv.Bp, g.AH2, dh, r0);
   sb_save(g.sv.dz3, g.sv.Bp, g.A, dz3, r0);

@@ -991,8 +991,9 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   a.cbh = L.c[CBH].off;
   a.cWo = L.c[CWO].off;
   a.cbo = L.c[CBO].off;
-  // all workgroups on one XCD (one L2 streams the weights) while they fit its
-  // 32 CUs: +3 % at C2 (profiles/r3/sb_xcd_ab_c2.txt)
+  // each role's workgroups on one XCD (one L2 streams the weights) while they
+  // fit its 32 CUs: +3 % at C2 (profiles/r3/sb_xcd_ab_c2.txt); phase 1's
+  // actor-forward workgroups are role 1, on the next XCD
   a.xstride = c->sb_xstride ? c->sb_xstride : (ceil_div(B, SB_R) <= 32 ? 8 : 1);
   return a;
 }
@@ -1023,8 +1024,12 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   const bool dp = c->comm != nullptr;
   float* const Gb = c->grad;
   {
-    ProfScope ps(c, "sb_phase1", 0, 4.0 * (double)G * (L.total + nc) + B * row_bytes);
-    hipLaunchKernelGGL(sb_phase1_kernel, dim3(G * a.xstride), dim3(SB_NT), c->sb_smem, c->cur, a);
+    // critic workgroups (role 0) stream both critics, the target actor and
+    // Wh^T; the actor-forward workgroups (role 1) the online actor
+    ProfScope ps(c, "sb_phase1", 0,
+                 4.0 * (double)G * (L.total + nc + na) + 2.0 * B * row_bytes);
+    const int grid = a.xstride > 1 ? G * a.xstride : 2 * G;
+    hipLaunchKernelGGL(sb_phase1_kernel, dim3(grid), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
   if (!dp) {
@@ -1038,7 +1043,9 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
     sb_wgrad(c, a, 1, G, 2, (double)nc);
   }
   {
-    ProfScope ps(c, "sb_phase3", 0, 4.0 * (double)G * (L.total + na) + B * c->S * 4.0);
+    ProfScope ps(c, "sb_phase3", 0,
+                 4.0 * (double)G * (nc + (double)c->CH1 * c->CH2 + (double)c->AH1 * c->AH2) +
+                     B * (c->S + c->A + c->AH1 + c->AH2) * 4.0);
     hipLaunchKernelGGL(sb_phase3_kernel, dim3(G * a.xstride), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
@@ -1115,18 +1122,18 @@ void sb_setup(ddpg_ctx* c) {
     if (const char* xv = getenv("DDPG_SB_XCD")) c->sb_xstride = atoi(xv) ? 8 : 1;
     const int G = ceil_div(c->sb_max_b, SB_R);
     const size_t Bp = (size_t)rup(c->sb_max_b, 4);
-    // saved tensors, feature-major [width][Bp]: xs xa cat dcat h dhp dq h1 h2 dz1 dz2 dz3
-    const size_t widths[12] = {(size_t)c->S, (size_t)c->A, 2 * (size_t)c->CH1,
+    // saved tensors, feature-major [width][Bp]: xs xa cat dcat h dhp dq h1 h2 dz1 dz2 dz3 o
+    const size_t widths[13] = {(size_t)c->S, (size_t)c->A, 2 * (size_t)c->CH1,
                                2 * (size_t)c->CH1, (size_t)c->CH2, (size_t)c->CH2, 1,
                                (size_t)c->AH1, (size_t)c->AH2, (size_t)c->AH1,
-                               (size_t)c->AH2, (size_t)c->A};
+                               (size_t)c->AH2, (size_t)c->A, (size_t)c->A};
     size_t tot = 0;
     for (size_t w : widths) tot += (Bp * w + 63) / 64 * 64;
     HIP_TRY(hipMalloc(&c->sb_save, tot * sizeof(float)));
     HIP_TRY(hipMemset(c->sb_save, 0, tot * sizeof(float)));
-    float* ptrs[12];
+    float* ptrs[13];
     size_t off = 0;
-    for (int k = 0; k < 12; ++k) {
+    for (int k = 0; k < 13; ++k) {
       ptrs[k] = c->sb_save + off;
       off += (Bp * widths[k] + 63) / 64 * 64;
     }
@@ -1144,6 +1151,7 @@ void sb_setup(ddpg_ctx* c) {
     sv.dz1 = ptrs[9];
     sv.dz2 = ptrs[10];
     sv.dz3 = ptrs[11];
+    sv.o = ptrs[12];
     const Layout& L = c->L;
     const int bp = (int)Bp;
     auto add = [bp](SbGradTab& t, const Tensor& ts, const float* X, const float* dY) {

@@ -152,6 +152,7 @@ struct SbSave {
   float *h, *dhp, *dq;     // [CH2],[CH2],[1] critic hidden, its pre-act grad, dQ
   float *h1, *h2;          // [AH1], [AH2]  actor hidden
   float *dz1, *dz2, *dz3;  // [AH1], [AH2], [A]
+  float* o;                // [A]           actor output tanh(.) (phase 1 -> phase 3)
 };
 
 // One network's weight-gradient table: tensor i occupies param offsets
