@@ -253,7 +253,7 @@ struct ddpg_ctx {
   float* sb_save = nullptr;   // per-row tensors the weight gradients read (SbSave)
   SbSave sb_sv{};
   SbGradTab sb_tab[2]{};      // weight-gradient tables: actor, critic
-  float* sb_misc = nullptr;   // alpha[2] | stat_part[2 * G]
+  float* sb_misc = nullptr;   // alpha[2] (of 4 floats)
   float* sb_whT = nullptr;    // [CH2][2 CH1] critic Wh^T shadow
   float* sb_w2T = nullptr;    // [AH2][AH1]   actor W2^T shadow
   bool sb_shadow_ok = false;  // cleared by every theta write outside the small path

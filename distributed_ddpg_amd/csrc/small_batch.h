@@ -92,7 +92,6 @@ struct SbArgs {
   SbSave sv;
   float* pw;             // beta powers [actor b1p, b2p, critic b1p, b2p]
   float* alpha;          // [actor, critic] Adam step sizes for this step
-  float* stat_part;      // [G][2] loss partial, q max
   float* stats;          // [q_max, loss]
   double* acc;           // [qmax_sum, loss_sum, steps]
   long long aW1, ab1, aW2, ab2, aW3;
@@ -430,10 +429,65 @@ DDPG_DEV void sb_actor_rows(const SbArgs& g, int r0, int valid, lds_f* red) {
   sb_save(g.sv.o, g.sv.Bp, g.A, o, r0);
 }
 
+// Phase 1's target workgroups: the TD target of the same rows (ddpg.py:90-97)
+// -- target actor forward at s2, target critic at (s2, mu'), y = t ? r : r +
+// gamma q' -- saved per row for the critic's weight-gradient kernel, which
+// forms dQ from it.  Nothing on the online chain waits for it inside the
+// launch, so it runs on CUs of its own.
+DDPG_DEV void sb_target_rows(const SbArgs& g, int r0, int valid, lds_f* red) {
+  const int tid = threadIdx.x;
+  const int LX = g.LX, LW = g.LW;
+  lds_f* xs2 = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
+  lds_f* ta2 = xs2 + 4 * LX;
+  lds_f* b1 = ta2 + 4 * LX;  // [LW][4] target h1, then target hh
+  lds_f* b2 = b1 + 4 * LW;   // target h2
+  lds_f* b3 = b2 + 4 * LW;   // target cat
+  lds_f* col = b3 + 4 * LW;  // [8][4]: q', r, t
+  const glb_f* T = GLB(g.target);
+  // the s2 rows as the online gather does (fp64 planes, scaler in fp64)
+  for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
+    const int k = idx >> 2, r = idx & 3;
+    float x2 = 0.f;
+    if (r < valid && k < g.S) {
+      const size_t e = (size_t)g.slots[r0 + r] * g.S + k;
+      const double x2d = g.rs2d ? g.rs2d[e] : (double)g.rs2[e];
+      x2 = g.mean ? (float)((x2d - g.mean[k]) / g.sdev[k]) : (float)x2d;
+    }
+    xs2[idx] = x2;
+  }
+  if (tid < 4) {
+    const bool ok = tid < valid;
+    const int sl = ok ? g.slots[r0 + tid] : 0;
+    col[1 * 4 + tid] = ok ? (g.rrd ? (float)g.rrd[sl] : g.rr[sl]) : 0.f;
+    col[2 * 4 + tid] = ok ? g.rt[sl] : 0.f;
+  }
+  __syncthreads();
+  {  // L1: target h1 | target state branch
+    const SbOp ops[2] = {sb_op(xs2, g.S, T + g.aW1, g.AH1, g.AH1, T + g.ab1, SB_ELU, b1),
+                         sb_op(xs2, g.S, T + g.cWs, g.CH1, g.CH1, T + g.cbs, SB_ELU, b3)};
+    const bool th[2] = {false, false};
+    sb_level<2>(ops, th, red);
+  }
+  // L2: target h2; L3: o' = tanh(h2' W3'), mu' = scale o'
+  sb_dense1(sb_op(b1, g.AH1, T + g.aW2, g.AH2, g.AH2, T + g.ab2, SB_ELU, b2), red);
+  sb_thin1(sb_op(b2, g.AH2, T + g.aW3, g.A, g.A, nullptr, SB_NONE, ta2), false, true, red);
+  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) ta2[idx] = __fmul_rn(ta2[idx], g.scale);
+  __syncthreads();
+  // L4: target action branch; L5: target critic hidden; L6: q'
+  sb_dense1(sb_op(ta2, g.A, T + g.cWa, g.CH1, g.CH1, T + g.cba, SB_ELU, b3 + 4 * g.CH1), red);
+  sb_dense1(sb_op(b3, 2 * g.CH1, T + g.cWh, g.CH2, g.CH2, T + g.cbh, SB_ELU, b1), red);
+  sb_thin1(sb_op(b1, g.CH2, T + g.cWo, 1, 1, T + g.cbo, SB_NONE, col), false, false, red);
+  // y = t ? r : r + gamma q'  (ddpg.py:92-97)
+  if (tid < valid) {
+    const float rr = col[1 * 4 + tid], tt = col[2 * 4 + tid];
+    g.sv.y[r0 + tid] = tt != 0.f ? rr : __fadd_rn(rr, __fmul_rn(g.gamma, col[tid]));
+  }
+}
+
 // Phase-1 roles: with XCD packing (xstride > 1) block b works as role b %
-// xstride (0: critic rows, 1: actor rows; the rest exit at once), so each
-// role's workgroups share one XCD's L2; otherwise blocks [0, G) are the
-// critic rows and [G, 2G) the actor rows.
+// xstride (0: online critic rows, 1: actor rows, 2: target rows; the rest
+// exit at once), so each role's workgroups share one XCD's L2; otherwise
+// blocks [role G, (role + 1) G) take role `role`.
 __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x;
@@ -446,47 +500,45 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
     role = blockIdx.x / G;
     wg = blockIdx.x - role * G;
   }
-  if (role > 1 || wg >= G) return;
+  if (role > 2 || wg >= G) return;
   const int r0 = wg * SB_R;
   const int valid = min(SB_R, g.B - r0);
   if (role == 1) {
     sb_actor_rows(g, r0, valid, LDS(sm));
     return;
   }
+  if (role == 2) {
+    sb_target_rows(g, r0, valid, LDS(sm));
+    return;
+  }
   const int LX = g.LX, LW = g.LW;
   lds_f* red = LDS(sm);
   lds_f* xs = red + SB_RED + 2 * SB_BIAS;  // [LX][4]
-  lds_f* xs2 = xs + 4 * LX;
-  lds_f* xa = xs2 + 4 * LX;
-  lds_f* ta2 = xa + 4 * LX;
-  lds_f* b1 = ta2 + 4 * LX;    // [LW][4] target h1, then target hh
-  lds_f* b2 = b1 + 4 * LW;     // target h2, then dhp
-  lds_f* b3 = b2 + 4 * LW;     // target cat, then dcat
-  lds_f* cat = b3 + 4 * LW;    // online cat
+  lds_f* xa = xs + 4 * LX;
+  lds_f* gh = xa + 4 * LX;     // [LW][4] dhp per unit dQ
+  lds_f* u = gh + 4 * LW;      // dcat per unit dQ
+  lds_f* cat = u + 4 * LW;     // online cat
   lds_f* h = cat + 4 * LW;     // online critic hidden
-  lds_f* col = h + 4 * LW;     // [8][4]: q', y, q, dq, r, t (feature-major too)
-  const glb_f* T = GLB(g.target);
+  lds_f* col = h + 4 * LW;     // [8][4]: q
   const glb_f* P = GLB(g.theta);
   SB_STAMP(0);
 
   if (wg == 0 && tid == 0) sb_alpha_and_advance(g.pw + 2, g.alpha + 1, g.lr_c, g.b1, g.b2);
-  // rows -> xs / xs2 / xa ([feature][4], zero past S / A and for rows past
-  // `valid`) in one pass: one slot read, then every ring read of an element in
-  // flight together; from the float64 ring planes when the ring keeps them; the
+  // rows -> xs / xa ([feature][4], zero past S / A and for rows past `valid`)
+  // in one pass: one slot read, then every ring read of an element in flight
+  // together; from the float64 ring planes when the ring keeps them; the
   // scaler (x - mean) / scale in fp64 before the one rounding to fp32 (the
-  // reference's preprocess_input + feed_dict cast); xs / xa also saved
-  // feature-major for the weight gradients
+  // reference's preprocess_input + feed_dict cast); also saved feature-major
+  // for the weight gradients
   for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
     const int k = idx >> 2, r = idx & 3;
-    float x = 0.f, x2 = 0.f, xv = 0.f;
+    float x = 0.f, xv = 0.f;
     if (r < valid) {
       const size_t sl = (size_t)g.slots[r0 + r];
       if (k < g.S) {
         const size_t e = sl * g.S + k;
         const double xd = g.rsd ? g.rsd[e] : (double)g.rs[e];
-        const double x2d = g.rs2d ? g.rs2d[e] : (double)g.rs2[e];
         x = g.mean ? (float)((xd - g.mean[k]) / g.sdev[k]) : (float)xd;
-        x2 = g.mean ? (float)((x2d - g.mean[k]) / g.sdev[k]) : (float)x2d;
         g.sv.xs[(size_t)k * g.sv.Bp + r0 + r] = x;
       }
       if (k < g.A) {
@@ -495,87 +547,37 @@ __global__ __launch_bounds__(SB_NT) void sb_phase1_kernel(SbArgs g) {
       }
     }
     xs[idx] = x;
-    xs2[idx] = x2;
     xa[idx] = xv;
-  }
-  if (tid < 4) {
-    const bool ok = tid < valid;
-    const int sl = ok ? g.slots[r0 + tid] : 0;
-    col[4 * 4 + tid] = ok ? (g.rrd ? (float)g.rrd[sl] : g.rr[sl]) : 0.f;
-    col[5 * 4 + tid] = ok ? g.rt[sl] : 0.f;
   }
   __syncthreads();
   SB_STAMP(1);
-  {  // L1: target h1 | target state branch | online state branch | online action branch
-    const SbOp ops[4] = {sb_op(xs2, g.S, T + g.aW1, g.AH1, g.AH1, T + g.ab1, SB_ELU, b1),
-                         sb_op(xs2, g.S, T + g.cWs, g.CH1, g.CH1, T + g.cbs, SB_ELU, b3),
-                         sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat),
+  {  // L1: online state branch | online action branch
+    const SbOp ops[2] = {sb_op(xs, g.S, P + g.cWs, g.CH1, g.CH1, P + g.cbs, SB_ELU, cat),
                          sb_op(xa, g.A, P + g.cWa, g.CH1, g.CH1, P + g.cba, SB_ELU,
                                cat + 4 * g.CH1)};
-    const bool th[4] = {false, false, false, false};
-    sb_level<4>(ops, th, red);
-  }
-  SB_STAMP(2);
-  {  // L2: target h2 | online critic hidden (networks.py:154-156)
-    const SbOp ops[2] = {sb_op(b1, g.AH1, T + g.aW2, g.AH2, g.AH2, T + g.ab2, SB_ELU, b2),
-                         sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_ELU, h)};
     const bool th[2] = {false, false};
     sb_level<2>(ops, th, red);
   }
+  SB_STAMP(2);
+  // L2: online critic hidden (networks.py:154-156); L3: q = h Wo + bo
+  sb_dense1(sb_op(cat, 2 * g.CH1, P + g.cWh, g.CH2, g.CH2, P + g.cbh, SB_ELU, h), red);
   SB_STAMP(3);
-  {  // L3: target actor out o' = tanh(h2' W3') | online q = h Wo + bo
-    SbOp ops[2] = {sb_op(b2, g.AH2, T + g.aW3, g.A, g.A, nullptr, SB_NONE, ta2),
-                   sb_op(h, g.CH2, P + g.cWo, 1, 1, P + g.cbo, SB_NONE, col + 2 * 4)};
-    ops[0].act_tanh = true;
-    const bool th[2] = {true, true};
-    sb_level<2>(ops, th, red);
-  }
-  for (int idx = tid; idx < 4 * g.A; idx += SB_NT) ta2[idx] = __fmul_rn(ta2[idx], g.scale);
-  __syncthreads();
+  sb_thin1(sb_op(h, g.CH2, P + g.cWo, 1, 1, P + g.cbo, SB_NONE, col), false, false, red);
   SB_STAMP(4);
-  // L4: target action branch; L5: target critic hidden; L6: q'
-  sb_dense1(sb_op(ta2, g.A, T + g.cWa, g.CH1, g.CH1, T + g.cba, SB_ELU, b3 + 4 * g.CH1), red);
-  SB_STAMP(5);
-  sb_dense1(sb_op(b3, 2 * g.CH1, T + g.cWh, g.CH2, g.CH2, T + g.cbh, SB_ELU, b1), red);
-  SB_STAMP(6);
-  sb_thin1(sb_op(b1, g.CH2, T + g.cWo, 1, 1, T + g.cbo, SB_NONE, col), false, false, red);
-  SB_STAMP(7);
-  // ---- y = t ? r : r + gamma q' (ddpg.py:92-97), MSE loss / dQ (networks.py:136):
-  // dq = -((1/B) * (2 * (y - q)))
-  if (tid == 0) {
-    float lsum = 0.f, qmax = -INFINITY;
-    for (int r = 0; r < 4; ++r) {
-      const float rr = col[4 * 4 + r], tt = col[5 * 4 + r];
-      const float y = tt != 0.f ? rr : __fadd_rn(rr, __fmul_rn(g.gamma, col[r]));
-      const float q = col[2 * 4 + r];
-      const float d = __fsub_rn(y, q);
-      const bool ok = r < valid;
-      const float dq = ok ? -__fmul_rn(g.inv_b, __fmul_rn(2.f, d)) : 0.f;
-      col[3 * 4 + r] = dq;
-      if (ok) {
-        g.sv.dq[r0 + r] = dq;
-        lsum += __fmul_rn(d, d);
-        qmax = fmaxf(qmax, q);
-      }
-    }
-    g.stat_part[wg * 2 + 0] = lsum;
-    g.stat_part[wg * 2 + 1] = qmax;
-  }
-  __syncthreads();
-  // ---- critic head backward: dhp = dq * Wo * elu'(h) -> b2
-  for (int idx = tid; idx < 4 * g.CH2; idx += SB_NT) {
-    const int j = idx >> 2, r = idx & 3;
-    b2[idx] = __fmul_rn(__fmul_rn(col[3 * 4 + r], P[g.cWo + j]), elu_grad_factor(h[idx]));
-  }
+  // ---- critic backward per unit dQ (networks.py:136's gradient, dQ = -(2/B)(y - q)
+  // applied by the weight-gradient kernel): gh = Wo * elu'(h); u = gh . Wh^T * elu'(cat)
+  for (int idx = tid; idx < 4 * g.CH2; idx += SB_NT)
+    gh[idx] = __fmul_rn(P[g.cWo + (idx >> 2)], elu_grad_factor(h[idx]));
   __syncthreads();
   SB_STAMP(8);
-  // L7: dcat = dhp . Wh^T * elu'(cat) -> b3   (Wh^T read from its row-major shadow)
-  sb_dense1(sb_op(b2, g.CH2, GLB(g.whT), 2 * g.CH1, 2 * g.CH1, nullptr, SB_AUX, b3, cat), red);
+  // L7 (Wh^T read from its row-major shadow)
+  sb_dense1(sb_op(gh, g.CH2, GLB(g.whT), 2 * g.CH1, 2 * g.CH1, nullptr, SB_AUX, u, cat), red);
   SB_STAMP(9);
+  if (tid < valid) g.sv.q[r0 + tid] = col[tid];
   sb_save(g.sv.cat, g.sv.Bp, 2 * g.CH1, cat, r0);
-  sb_save(g.sv.dcat, g.sv.Bp, 2 * g.CH1, b3, r0);
+  sb_save(g.sv.dcat, g.sv.Bp, 2 * g.CH1, u, r0);
   sb_save(g.sv.h, g.sv.Bp, g.CH2, h, r0);
-  sb_save(g.sv.dhp, g.sv.Bp, g.CH2, b2, r0);
+  sb_save(g.sv.dhp, g.sv.Bp, g.CH2, gh, r0);
   SB_STAMP_SYNC(10);
 }
 
@@ -725,12 +727,43 @@ constexpr int SB_GU = 16;  // float4s (4 batch rows each) per batch of loads
 // gradient only (the critic call stores this rank's {max Q, loss share} to
 // g.stats for the all-gather, no running sums); mode 2 reads the summed
 // gradient back and applies Adam, the soft update and the shadow.
+//
+// The critic's call forms dQ = -((1/B) * (2 * (y - q))) per row (the MSE
+// gradient, networks.py:136, from phase 1's saved q and TD target) into LDS
+// first; its tensors' saved output gradients are per unit dQ (sdq), scaled
+// by dQ[b] as they are read.  Its block 0 also forms the step stats: loss
+// partials and max Q per 4-row group in row order, then summed in group order.
+constexpr int SB_MAXB = 512;  // rows of the small path (sb_setup's sb_max_b)
 __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTab tab, int net,
                                                               int nslab, int mode) {
 #ifdef DDPG_SB_STAMPS
   const int sbase = net == 1 ? 48 : 56;
 #endif
   SB_STAMP(sbase);
+  __shared__ __attribute__((aligned(16))) float dqs[SB_MAXB];
+  __shared__ float sp[2][SB_MAXB / SB_R];
+  const bool crit = net == 1 && mode != 2;  // grid-uniform
+  if (crit) {
+    for (int b = threadIdx.x; b < ((g.B + 3) & ~3); b += SB_GT) {
+      float dq = 0.f;
+      if (b < g.B) dq = -__fmul_rn(g.inv_b, __fmul_rn(2.f, __fsub_rn(g.sv.y[b], g.sv.q[b])));
+      dqs[b] = dq;
+    }
+    if (blockIdx.x == 0) {
+      for (int w = threadIdx.x; w < nslab; w += SB_GT) {
+        float lsum = 0.f, qmax = -INFINITY;
+        for (int r = 0; r < SB_R && w * SB_R + r < g.B; ++r) {
+          const float q = g.sv.q[w * SB_R + r];
+          const float d = __fsub_rn(g.sv.y[w * SB_R + r], q);
+          lsum += __fmul_rn(d, d);
+          qmax = fmaxf(qmax, q);
+        }
+        sp[0][w] = lsum;
+        sp[1][w] = qmax;
+      }
+    }
+    __syncthreads();
+  }
   int ti = 0;
 #pragma unroll
   for (int i = 1; i < SB_MAXT; ++i)
@@ -752,7 +785,9 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     t0 = g.target[i];
   }
   const f32x4* xp = T.X ? reinterpret_cast<const f32x4*>(T.X + (size_t)kc * T.ldx) : nullptr;
-  const f32x4* dp = reinterpret_cast<const f32x4*>(T.dY + (size_t)nc * T.ldy);
+  const f32x4* dp = T.dY ? reinterpret_cast<const f32x4*>(T.dY + (size_t)nc * T.ldy) : nullptr;
+  const lds_v4* dq4 = reinterpret_cast<const lds_v4*>(LDS(dqs));
+  const bool sdq = crit && T.sdq;
   const int nq = mode == 2 ? 0 : (g.B + 3) >> 2;
   float gv = mode == 2 ? g.grad[i] : 0.f;
   for (int q0 = 0; q0 < nq; q0 += SB_GU) {
@@ -761,7 +796,15 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     for (int u = 0; u < SB_GU; ++u) {
       const int qq = min(q0 + u, nq - 1);
       xv[u] = xp ? xp[qq] : f32x4{1.f, 1.f, 1.f, 1.f};
-      dv[u] = dp[qq];
+      dv[u] = dp ? dp[qq] : f32x4{1.f, 1.f, 1.f, 1.f};
+    }
+    if (sdq) {
+#pragma unroll
+      for (int u = 0; u < SB_GU; ++u) {
+        const f32x4 d = dq4[min(q0 + u, nq - 1)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dv[u][e] = __fmul_rn(d[e], dv[u][e]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < SB_GU; ++u)
@@ -786,20 +829,11 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     if (ti == tab.shadow) tab.sh[(size_t)n * T.K + k] = p;
   }
   SB_STAMP(sbase + 2);
-  if (net == 1 && mode != 2 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (crit && blockIdx.x == 0 && threadIdx.x == 0) {
     float ls = 0.f, qm = -INFINITY;
-    for (int w0 = 0; w0 < nslab; w0 += 8) {  // in order, 8 loads in flight
-      f32x2v v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = w0 + u < nslab ? f32x2v{g.stat_part[2 * (w0 + u)], g.stat_part[2 * (w0 + u) + 1]}
-                              : f32x2v{0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (w0 + u < nslab) {
-          ls += v[u][0];
-          qm = fmaxf(qm, v[u][1]);
-        }
+    for (int w = 0; w < nslab; ++w) {  // in group order
+      ls += sp[0][w];
+      qm = fmaxf(qm, sp[1][w]);
     }
     const float loss = __fmul_rn(ls, g.inv_b);
     g.stats[0] = qm;

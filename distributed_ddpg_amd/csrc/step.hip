@@ -975,7 +975,6 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   a.sv = c->sb_sv;
   a.pw = c->dpw;
   a.alpha = c->sb_misc;
-  a.stat_part = c->sb_misc + 4;
   a.stats = c->dstats;
   a.acc = c->dacc;
   a.aW1 = L.a[AW1].off;
@@ -993,7 +992,7 @@ static SbArgs sb_args(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
   a.cbo = L.c[CBO].off;
   // each role's workgroups on one XCD (one L2 streams the weights) while they
   // fit its 32 CUs: +3 % at C2 (profiles/r3/sb_xcd_ab_c2.txt); phase 1's
-  // actor-forward workgroups are role 1, on the next XCD
+  // three roles take XCDs 0, 1, 2
   a.xstride = c->sb_xstride ? c->sb_xstride : (ceil_div(B, SB_R) <= 32 ? 8 : 1);
   return a;
 }
@@ -1024,11 +1023,12 @@ static void learner_step_small(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b)
   const bool dp = c->comm != nullptr;
   float* const Gb = c->grad;
   {
-    // critic workgroups (role 0) stream both critics, the target actor and
-    // Wh^T; the actor-forward workgroups (role 1) the online actor
+    // three sets of workgroups: online critic rows (role 0: the online
+    // critic and Wh^T), actor rows (1: the online actor), target rows (2: the
+    // target actor and critic)
     ProfScope ps(c, "sb_phase1", 0,
                  4.0 * (double)G * (L.total + nc + na) + 2.0 * B * row_bytes);
-    const int grid = a.xstride > 1 ? G * a.xstride : 2 * G;
+    const int grid = a.xstride > 1 ? G * a.xstride : 3 * G;
     hipLaunchKernelGGL(sb_phase1_kernel, dim3(grid), dim3(SB_NT), c->sb_smem, c->cur, a);
     HIP_TRY(hipGetLastError());
   }
@@ -1117,23 +1117,23 @@ void sb_setup(ddpg_ctx* c) {
             c->CH1 % 4 == 0 && c->CH2 % 4 == 0 && smem <= 160 * 1024;
   if (const char* sv = getenv("DDPG_SMALL")) ok = ok && atoi(sv) != 0;
   if (ok) {
-    c->sb_max_b = std::min(c->Bmax, 512);
+    c->sb_max_b = std::min(c->Bmax, SB_MAXB);
     c->sb_smem = smem;
     if (const char* xv = getenv("DDPG_SB_XCD")) c->sb_xstride = atoi(xv) ? 8 : 1;
-    const int G = ceil_div(c->sb_max_b, SB_R);
     const size_t Bp = (size_t)rup(c->sb_max_b, 4);
-    // saved tensors, feature-major [width][Bp]: xs xa cat dcat h dhp dq h1 h2 dz1 dz2 dz3 o
-    const size_t widths[13] = {(size_t)c->S, (size_t)c->A, 2 * (size_t)c->CH1,
+    // saved tensors, feature-major [width][Bp]:
+    // xs xa cat dcat h dhp q h1 h2 dz1 dz2 dz3 o y
+    const size_t widths[14] = {(size_t)c->S, (size_t)c->A, 2 * (size_t)c->CH1,
                                2 * (size_t)c->CH1, (size_t)c->CH2, (size_t)c->CH2, 1,
                                (size_t)c->AH1, (size_t)c->AH2, (size_t)c->AH1,
-                               (size_t)c->AH2, (size_t)c->A, (size_t)c->A};
+                               (size_t)c->AH2, (size_t)c->A, (size_t)c->A, 1};
     size_t tot = 0;
     for (size_t w : widths) tot += (Bp * w + 63) / 64 * 64;
     HIP_TRY(hipMalloc(&c->sb_save, tot * sizeof(float)));
     HIP_TRY(hipMemset(c->sb_save, 0, tot * sizeof(float)));
-    float* ptrs[13];
+    float* ptrs[14];
     size_t off = 0;
-    for (int k = 0; k < 13; ++k) {
+    for (int k = 0; k < 14; ++k) {
       ptrs[k] = c->sb_save + off;
       off += (Bp * widths[k] + 63) / 64 * 64;
     }
@@ -1145,17 +1145,20 @@ void sb_setup(ddpg_ctx* c) {
     sv.dcat = ptrs[3];
     sv.h = ptrs[4];
     sv.dhp = ptrs[5];
-    sv.dq = ptrs[6];
+    sv.q = ptrs[6];
     sv.h1 = ptrs[7];
     sv.h2 = ptrs[8];
     sv.dz1 = ptrs[9];
     sv.dz2 = ptrs[10];
     sv.dz3 = ptrs[11];
     sv.o = ptrs[12];
+    sv.y = ptrs[13];
     const Layout& L = c->L;
     const int bp = (int)Bp;
-    auto add = [bp](SbGradTab& t, const Tensor& ts, const float* X, const float* dY) {
+    auto add = [bp](SbGradTab& t, const Tensor& ts, const float* X, const float* dY,
+                    int sdq = 0) {
       SbGradT& e = t.t[t.n];
+      e.sdq = sdq;
       e.off = (long long)ts.off;
       e.K = ts.cols == 1 && X == nullptr ? 1 : ts.rows;
       e.N = ts.cols == 1 && X == nullptr ? ts.rows : ts.cols;
@@ -1187,18 +1190,19 @@ void sb_setup(ddpg_ctx* c) {
     ta.shadow = 2;
     SbGradTab& tc = c->sb_tab[1];  // critic (networks.py:130-137)
     tc.n = 0;
-    add(tc, L.c[CWS], sv.xs, sv.dcat);
-    add(tc, L.c[CBS], nullptr, sv.dcat);
-    add(tc, L.c[CWA], sv.xa, sv.dcat + (size_t)c->CH1 * Bp);
-    add(tc, L.c[CBA], nullptr, sv.dcat + (size_t)c->CH1 * Bp);
-    add(tc, L.c[CWH], sv.cat, sv.dhp);
-    add(tc, L.c[CBH], nullptr, sv.dhp);
-    add(tc, L.c[CWO], sv.h, sv.dq);
-    add(tc, L.c[CBO], nullptr, sv.dq);
+    // (the saved dcat / dhp are per unit dQ; dQ itself formed in the kernel)
+    add(tc, L.c[CWS], sv.xs, sv.dcat, 1);
+    add(tc, L.c[CBS], nullptr, sv.dcat, 1);
+    add(tc, L.c[CWA], sv.xa, sv.dcat + (size_t)c->CH1 * Bp, 1);
+    add(tc, L.c[CBA], nullptr, sv.dcat + (size_t)c->CH1 * Bp, 1);
+    add(tc, L.c[CWH], sv.cat, sv.dhp, 1);
+    add(tc, L.c[CBH], nullptr, sv.dhp, 1);
+    add(tc, L.c[CWO], sv.h, nullptr, 1);
+    add(tc, L.c[CBO], nullptr, nullptr, 1);
     close(tc);
     tc.shadow = 4;
-    HIP_TRY(hipMalloc(&c->sb_misc, (4 + 2 * (size_t)G) * sizeof(float)));
-    HIP_TRY(hipMemset(c->sb_misc, 0, (4 + 2 * (size_t)G) * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->sb_misc, 4 * sizeof(float)));
+    HIP_TRY(hipMemset(c->sb_misc, 0, 4 * sizeof(float)));
     HIP_TRY(hipMalloc(&c->sb_whT, (size_t)2 * c->CH1 * c->CH2 * sizeof(float)));
     HIP_TRY(hipMalloc(&c->sb_w2T, (size_t)c->AH1 * c->AH2 * sizeof(float)));
     ta.sh = c->sb_w2T;

@@ -149,7 +149,8 @@ struct SbSave {
   int Bp;
   float *xs, *xa;          // [S], [A]      inputs (scaled)
   float *cat, *dcat;       // [2 CH1]       critic concat, its gradient
-  float *h, *dhp, *dq;     // [CH2],[CH2],[1] critic hidden, its pre-act grad, dQ
+  float *h, *dhp;          // [CH2],[CH2]   critic hidden, its pre-act grad / dQ (below)
+  float *q, *y;            // [1], [1]      online Q, TD target (ddpg.py:92-97)
   float *h1, *h2;          // [AH1], [AH2]  actor hidden
   float *dz1, *dz2, *dz3;  // [AH1], [AH2], [A]
   float* o;                // [A]           actor output tanh(.) (phase 1 -> phase 3)
@@ -159,7 +160,9 @@ struct SbSave {
 // [off, off + K*N) (row-major [K][N]); its gradient is
 //   g[k][n] = sum_b X[k][b] dY[n][b]   (feature-major saves; X == nullptr: bias, X = 1)
 // over the B saved rows, computed by tiles of TK x TN elements (TK*TN = SB_GT)
-// starting at block tile0.
+// starting at block tile0.  sdq: the saved dY is the critic's output
+// gradient per unit dQ, and dY[n][b] = dQ[b] * saved[n][b] (dY == nullptr:
+// dQ itself), dQ formed in the kernel from the saved q and TD target.
 struct SbGradT {
   long long off;
   int K, N;
@@ -168,6 +171,7 @@ struct SbGradT {
   const float* dY;
   int ldy;
   int TN, TK, tile0;
+  int sdq;
 };
 constexpr int SB_MAXT = 10;  // tensors per network + the sentinel
 struct SbGradTab {
