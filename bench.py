@@ -336,6 +336,14 @@ def kernel_profile(fl, sess, steps):
     return rows, wall
 
 
+# A pack launch runs the same kernel body as the single launch over up to
+# GH_MAXP independent GEMMs (csrc/gemm_h3.h, gemm_h3m.h): the roofline rates
+# that body, so its pack launches count with it (launches, FLOP, time added;
+# the members and their launches per step are listed in the record).
+BODY_OF = {"gemm_h3m_pack_kernel<RK,KR,NP=3>": "gemm_h3m_kernel<RK,KR,NP=3>",
+           "gemm_h16i_pack_kernel<RK,KR,NP=1>": "gemm_h16i_kernel<RK,KR,NP=1>"}
+
+
 def summarize_profile(rows, steps):
     by_kernel = {}
     for key, r in rows.items():
@@ -343,11 +351,18 @@ def summarize_profile(rows, steps):
         k = by_kernel.setdefault(sym, {"ms": 0.0, "launches": 0, "flops": 0.0, "bytes": 0.0})
         for f in ("ms", "launches", "flops", "bytes"):
             k[f] += r[f]
+    bodies = {}
+    for sym, r in by_kernel.items():
+        k = bodies.setdefault(BODY_OF.get(sym, sym), {"ms": 0.0, "launches": 0, "flops": 0.0,
+                                                      "bytes": 0.0, "members": {}})
+        for f in ("ms", "launches", "flops", "bytes"):
+            k[f] += r[f]
+        k["members"][sym] = r["launches"] / steps
     # the collectives' events run on the comm stream concurrently with kernels,
     # and the xwin records are exchange-overlap windows (spans of the step):
     # neither is GPU-busy time nor a roofline candidate
     side = ("rccl", "xwin")
-    comp = {k: v for k, v in by_kernel.items() if not k.startswith(side)}
+    comp = {k: v for k, v in bodies.items() if not k.startswith(side)}
     gpu_ms = sum(r["ms"] for k, r in rows.items() if not k.startswith(side)) / steps
     gemm_ms = sum(r["ms"] for k, r in comp.items() if k.startswith("gemm")) / steps
     gemm_flops = sum(r["flops"] for k, r in comp.items() if k.startswith("gemm")) / steps
@@ -389,6 +404,20 @@ def pmc_traffic(cfg_name, kernel, launches_per_step):
                 os.path.relpath(fn, ROOT), lps, launches_per_step)
         return round(k["traffic_bytes_per_launch"]), os.path.relpath(fn, ROOT)
     return None, None
+
+
+def body_traffic(cfg_name, dom):
+    """pmc_traffic of a kernel body: the launch-weighted mean over its members
+    (single and pack launches), each checked against its launches per step."""
+    tot, n, srcs = 0.0, 0.0, []
+    for sym, lps in dom["members"].items():
+        t, src = pmc_traffic(cfg_name, sym, lps)
+        if t is None:
+            return None, src
+        tot += t * lps
+        n += lps
+        srcs.append(src)
+    return (round(tot / n) if n else None), ", ".join(sorted(set(srcs)))
 
 
 def kernel_peak(name):
@@ -734,7 +763,7 @@ def main():
     # the pipe the step's GEMMs run on: bf16 operands at 2.5 PF; fp32 contexts
     # on the same bf16 pipe at six plane products per MAC (2.5 PF / 6)
     step_peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_S3_FP32EQ_TFLOPS
-    traffic, traffic_src = (pmc_traffic(cfg, dom_name, dom["launches"] / args.profile_steps)
+    traffic, traffic_src = (body_traffic(cfg, dom)
                             if world == 1 else (None, "PMC passes are single-GPU"))
     roofline = {"bound": "mfma", "kernel": dom_name, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
@@ -744,7 +773,7 @@ def main():
                 "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
                 "avg_launch_us": round(dom_avg_ms * 1e3, 2),
                 "flop_per_launch": dom_flops, "launches_per_step":
-                    dom["launches"] / args.profile_steps}
+                    dom["launches"] / args.profile_steps, "launches": dom["members"]}
     metric = ("actor+critic updates/sec (global batch %d, %d-wide MLPs)" % (B0, H1) if strong else
               "actor+critic updates/sec (batch %d per GPU, %d-wide MLPs)" % (B, H1))
     out = {
@@ -851,7 +880,7 @@ def main():
         ms5 = 1000.0 * el5 / 30
         ach5 = (d5["flops"] / d5["launches"]) / (d5["ms"] / d5["launches"] * 1e-3) / 1e12
         pk5 = kernel_peak(dn5)
-        tr5, tr5_src = pmc_traffic("c5", dn5, d5["launches"] / 10) if world == 1 else (None, None)
+        tr5, tr5_src = body_traffic("c5", d5) if world == 1 else (None, None)
         out["c5_bf16"] = {
             "workload": label5 + ", bf16 GEMM operands (fp32 master weights/accumulation)",
             "value": round((1 if strong else world) * 30 / el5, 3), "unit": "updates/s",
@@ -865,7 +894,7 @@ def main():
                          "unit": "TFLOP/s", "frac": round(ach5 / pk5, 4), "traffic": tr5,
                          "traffic_source": tr5_src,
                          "avg_launch_us": round(1e3 * d5["ms"] / d5["launches"], 2),
-                         "launches_per_step": d5["launches"] / 10},
+                         "launches_per_step": d5["launches"] / 10, "launches": d5["members"]},
             "kernels": {k: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
                             "per_step": v["launches"] / 10}
                         for k, v in sorted(bk5.items(), key=lambda kv: -kv[1]["ms"])}}

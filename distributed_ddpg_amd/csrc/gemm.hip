@@ -381,8 +381,11 @@ GemmPlan gemm_launch(ddpg_ctx* c, const char* name, const float* A, int lda,
       const double fl = 2.0 * M * N * (double)K,
                    by = 2.0 * c->hnp * ((double)M * K + (double)K * N) + 4.0 * (double)M * N * h.splits;
       if constexpr (AL == L_RK && BL == L_KR) {
-        // gemm_defer (first_layers_dev): queue for one gemm_h16i_pack_kernel launch
-        if (c->gemm_defer && h16 && c->sw.gemm_h3 && h.splits == 1 && !a.kpart) {
+        // gemm_defer (first_layers_dev, learner_step_dev's forward layers):
+        // queue for one pack launch -- the kernels with a pack form only
+        // (gemm_h16i, gemm_h3m)
+        const bool pk_ok = h16 ? c->sw.gemm_h3 : (c->sw.gemm_h3 && m16);
+        if (c->gemm_defer && pk_ok && h.splits == 1 && !a.kpart) {
           DeferredGemm d;
           d.a = a;
           d.grid = grid;
@@ -521,16 +524,21 @@ void gemm_flush(ddpg_ctx* c) {
     while (c->sw.gemm_pack && i + n < q.size() && n < (size_t)GH_MAXP &&
            q[i + n].grid.x == q[i].grid.x && q[i + n].grid.y == q[i].grid.y)
       ++n;
+    const bool f3 = c->hnp == 3;  // fp32 context: gemm_h3m (else gemm_h16i)
     if (n == 1) {
       ProfScope ps(c, q[i].key, q[i].flops, q[i].bytes);
-      hipLaunchKernelGGL((gemm_h16i_kernel<L_RK, L_KR>), q[i].grid, dim3(HG_NT), 0, c->cur, q[i].a);
+      if (f3)
+        hipLaunchKernelGGL((gemm_h3m_kernel<L_RK, L_KR>), q[i].grid, dim3(HG_NT), 0, c->cur, q[i].a);
+      else
+        hipLaunchKernelGGL((gemm_h16i_kernel<L_RK, L_KR>), q[i].grid, dim3(HG_NT), 0, c->cur,
+                           q[i].a);
     } else {
       GemmHPack pk;
       double fl = 0, by = 0;
       // gemm_hw_pack_kernel (two 4-wave blocks per CU) when every part is a
       // full-tile forward layer (bias, elu; twin and / or fp32 out) of whole
       // 64-deep steps
-      bool hw = c->sw.gemm_hw;
+      bool hw = c->sw.gemm_hw && !f3;
       for (size_t j = 0; j < n; ++j) {
         pk.p[j] = q[i + j].a;
         fl += q[i + j].flops;
@@ -542,10 +550,14 @@ void gemm_flush(ddpg_ctx* c) {
              !e.nw_out[0] && !e.nw_out[1] && !e.out_split_stride;
       }
       char key[128];
-      snprintf(key, sizeof key, "%s<RK,KR,NP=1>|%s",
-               hw ? "gemm_hw_pack_kernel" : "gemm_h16i_pack_kernel", strchr(q[i].key, '|') + 1);
+      snprintf(key, sizeof key, "%s<RK,KR,NP=%d>|%s",
+               f3 ? "gemm_h3m_pack_kernel" : hw ? "gemm_hw_pack_kernel" : "gemm_h16i_pack_kernel",
+               c->hnp, strchr(q[i].key, '|') + 1);
       ProfScope ps(c, key, fl, by);
-      if (hw)
+      if (f3)
+        hipLaunchKernelGGL((gemm_h3m_pack_kernel<L_RK, L_KR>), dim3(q[i].grid.x, q[i].grid.y, n),
+                           dim3(HG_NT), 0, c->cur, pk);
+      else if (hw)
         hipLaunchKernelGGL((gemm_hw_pack_kernel<L_RK, L_KR, HG_BN, 2, 64, 1>),
                            dim3(q[i].grid.x, q[i].grid.y, n), dim3(2 * HG_BN), 0, c->cur, pk);
       else

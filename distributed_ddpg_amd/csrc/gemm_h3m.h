@@ -36,7 +36,7 @@
 namespace ddpg {
 
 template <int AL, int BL>
-__global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
+DDPG_DEV void gemm_h3m_body(const GemmHArgs& g, int z) {
   KC_STAMP(0)
   constexpr int NP = 3, BM = 128, BK = 32;
   using C = HgCfg<BM, BK, NP, 8>;
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
   int bx, by;
   xcd_tile(bx, by, g.xcd);
-  const int n0 = bx * HG_BN, m0 = by * BM, z = blockIdx.z;
+  const int n0 = bx * HG_BN, m0 = by * BM;
   const int kbeg = z * g.kps;
   const int kend = min(g.K, kbeg + g.kps);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
@@ -323,6 +323,22 @@ __global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
                 "epilogue LDS (+ the narrow rows of a fused weight gradient)");
   gemm_epilogue<BM, HG_BN, 4, 16, BM>(out, smem, ge, tid, n0, m0, ze, bx, by);
   KC_STAMP(3)
+}
+
+template <int AL, int BL>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_kernel(GemmHArgs g) {
+  gemm_h3m_body<AL, BL>(g, blockIdx.z);
+}
+
+// Up to GH_MAXP independent GEMMs of one grid shape in one launch, part =
+// blockIdx.z (one split each, no in-launch combine): the fp32 context's
+// forward layers that read only the first layers' outputs (target actor W2,
+// online actor W2, online critic Wh; learner_step_dev).  A CU's next block,
+// the next part's tile, starts while the previous block's epilogue drains,
+// instead of each launch's ramp and tail on its own.
+template <int AL, int BL>
+__global__ __launch_bounds__(HG_NT, 1) void gemm_h3m_pack_kernel(GemmHPack pk) {
+  gemm_h3m_body<AL, BL>(pk.p[blockIdx.z], 0);
 }
 
 }  // namespace ddpg

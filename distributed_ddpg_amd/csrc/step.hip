@@ -90,6 +90,33 @@ static TkPart actor_l1_part(ddpg_ctx* c, const float* base, const float* s, int 
   return tp;
 }
 
+// The actor's layer 2 (networks.py:57-60) with the W3 projection partials of
+// the output layer in its epilogue (into c->ppart); h2 stored when non-null.
+static GemmPlan actor_l2(ddpg_ctx* c, const float* base, int B, const float* h1, float* h2) {
+  const Layout& L = c->L;
+  GemmEpi e = epi_none();
+  e.out = h2;
+  e.ldo = c->ldAH2;
+  e.bias = P(c, base, L.a[AB2]);
+  e.act = 1;
+  e.proj = P(c, base, L.a[AW3]);
+  e.proj_n = c->A;
+  e.proj_sn = c->A;
+  e.proj_sa = 1;
+  e.proj_out = c->ppart;
+  return gemm_launch<L_RK, L_KR>(c, "fwd_head", h1, c->ldAH1, P(c, base, L.a[AW2]), c->AH2, B,
+                                 c->AH2, c->AH1, e);
+}
+
+// o = tanh(sum of the nt projection partials in c->ppart), mu = scale o
+// (networks.py:61-63)
+static void actor_out_launch(ddpg_ctx* c, int nt, int B, float* o, float* mu) {
+  ProfScope ps(c, "actor_out", 0, 0);
+  hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->cur,
+                     c->ppart, nt, B, c->A, c->cfg.action_scale, o, mu, c->ldA);
+  HIP_TRY(hipGetLastError());
+}
+
 // Actor forward (networks.py:51-63) on [B][ldS] states.
 // h1 is always materialised (input of layer 2); h2 only when h2 != nullptr.
 // l1_done: h1 was already produced (first_layers_dev).
@@ -110,22 +137,8 @@ static void actor_fwd(ddpg_ctx* c, const float* base, const float* s, int B, flo
     gemm_launch<L_RK, L_KR>(c, "fwd", s, c->ldS, P(c, base, L.a[AW1]), c->AH1, B, c->AH1, c->S,
                             e);
   }
-  e = epi_none();
-  e.out = h2;
-  e.ldo = c->ldAH2;
-  e.bias = P(c, base, L.a[AB2]);
-  e.act = 1;
-  e.proj = P(c, base, L.a[AW3]);
-  e.proj_n = c->A;
-  e.proj_sn = c->A;
-  e.proj_sa = 1;
-  e.proj_out = c->ppart;
-  GemmPlan pl = gemm_launch<L_RK, L_KR>(c, "fwd_head", h1, c->ldAH1, P(c, base, L.a[AW2]),
-                                        c->AH2, B, c->AH2, c->AH1, e);
-  ProfScope ps(c, "actor_out", 0, 0);
-  hipLaunchKernelGGL(actor_out_kernel, dim3(ceil_div(B * c->A, 256)), dim3(256), 0, c->cur,
-                     c->ppart, pl.nt(c->AH2), B, c->A, c->cfg.action_scale, o, mu, c->ldA);
-  HIP_TRY(hipGetLastError());
+  const GemmPlan pl = actor_l2(c, base, B, h1, h2);
+  actor_out_launch(c, pl.nt(c->AH2), B, o, mu);
 }
 
 // Critic first layer + hidden layer (networks.py:147-161).  mode:
@@ -873,6 +886,35 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   // ddpg.py:90-109's batch-only first layers, all at once (every later use
   // reads them with the same pre-step parameters)
   const bool l1 = first_layers_dev(c, B);
+  const bool mu_in_window = c->comm && !c->par;
+  if (l1 && !c->par && !mu_in_window && c->sw.fwd_pack) {
+    // The three layers that read only the first layers' outputs -- target
+    // actor W2 (ddpg.py:90), online actor W2 (ddpg.py:106) and online critic
+    // Wh (ddpg.py:100) -- as ONE pack launch (gemm_flush: a CU starts the next
+    // part's tile while the previous tile's epilogue drains), then what
+    // depends on them.  Same buffers, same per-tile arithmetic as the
+    // sequential order below (DDPG_FWD_PACK=0): bitwise equal.
+    c->gemm_defer = 1;
+    std::swap(c->ppart, c->ppart_t);
+    const GemmPlan pt = actor_l2(c, c->target, B, c->th1, nullptr);
+    std::swap(c->ppart, c->ppart_t);
+    const GemmPlan po = actor_l2(c, c->theta, B, c->h1, c->h2);
+    const int nq = critic_fwd(c, c->theta, c->s, c->a, B, c->cat, c->h, 0, nullptr, 2);
+    c->gemm_defer = 0;
+    gemm_flush(c);
+    // mu' = actor.predict_target(s2), then critic.predict_target(s2, mu')
+    std::swap(c->ppart, c->ppart_t);
+    std::swap(c->qpart, c->qpart_t);
+    actor_out_launch(c, pt.nt(c->AH2), B, nullptr, c->ta2);
+    c->td_nqt = critic_fwd(c, c->target, c->s2, c->ta2, B, c->tcat, nullptr, 1, nullptr, 1);
+    std::swap(c->ppart, c->ppart_t);
+    std::swap(c->qpart, c->qpart_t);
+    actor_out_launch(c, po.nt(c->AH2), B, c->o, c->mu);  // a_outs (ddpg.py:106)
+    critic_train_dev(c, B, inv_b, true, nq, false);
+    critic_action_grad(c, c->s, c->mu, B, nullptr, c->dz3, c->o);
+    actor_train_dev(c, B, true, false);
+    return;
+  }
   fork_to(c, 0, s0, s1);
   fork_to(c, 0, s0, s2);
   // target_q = critic.predict_target(s2, actor.predict_target(s2))  ddpg.py:90
@@ -891,7 +933,6 @@ static void learner_step_dev(ddpg_ctx* c, int B, float inv_b) {
   // actor.train).  Data-parallel step on one stream: issued inside the
   // critic's exchange window instead (it reads no critic parameter), so the
   // critic's tail all-reduce runs under it rather than in front of Adam.
-  const bool mu_in_window = c->comm && !c->par;
   auto online_actor_fwd = [&] { actor_fwd(c, c->theta, c->s, B, c->h1, c->h2, c->o, c->mu, l1); };
   if (!mu_in_window) {
     c->cur = s2;

@@ -45,6 +45,10 @@ def bench_name(rocprof_name):
     a[0], a[1] = lay.get(a[0], a[0]), lay.get(a[1], a[1])
     if sym == "gemm_h16i_pack_kernel" and len(a) == 2:
         return "%s<%s,%s,NP=1>" % (sym, a[0], a[1])
+    if sym == "gemm_h3m_pack_kernel" and len(a) == 2:
+        return "%s<%s,%s,NP=3>" % (sym, a[0], a[1])
+    if sym in ("gemm_hw_kernel", "gemm_hw_pack_kernel"):  # bf16 (one plane) by construction
+        return "%s<%s,%s,NP=1>" % (sym, a[0], a[1])
     if sym == "gemm_s3_kernel" and len(a) == 3:
         # bench.py labels the one-plane instantiation gemm_bf16_kernel
         return "%s<%s,%s>" % ("gemm_s3_kernel" if a[2] == "3" else "gemm_bf16_kernel", a[0], a[1])

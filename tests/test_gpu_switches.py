@@ -65,7 +65,8 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_SLOTS_H2D", "DDPG_GRAPH_AUTO", "DDPG_KCOMB", "DDPG_KCOMB_BLOCKS",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
-            "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW")
+            "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW",
+            "DDPG_FWD_PACK")
 
 
 @pytest.fixture(scope="module")
@@ -217,6 +218,25 @@ def test_gemm_pack_bf16_bitwise(dd, O, monkeypatch):
     got = _run(dd, O, "wides", p, 2, dtype="bf16", profile=True)
     assert not any("pack_kernel" in k for k in got["keys"]), got["keys"]
     _bitwise(got_h16, ref)
+    _bitwise(got, ref)
+
+
+@pytest.mark.parametrize("name,dtype,kern", [("wide", "fp32", "gemm_h3m_pack_kernel"),
+                                              ("wides", "bf16", "gemm_h16i_pack_kernel")])
+def test_fwd_pack_bitwise(dd, O, monkeypatch, name, dtype, kern):
+    """The step's three forward layers that read only the first layers'
+    outputs (target actor W2, online actor W2, online critic Wh) as one pack
+    launch by default, and in the sequential order with DDPG_FWD_PACK=0: the
+    same kernel body per tile, the same buffers -- bitwise equal after 2 fused
+    steps.  DDPG_KCOMB=0 keeps B = 256 on the unsplit plan the pack takes."""
+    _clear(monkeypatch)
+    monkeypatch.setenv("DDPG_KCOMB", "0")
+    p, _ = _params(O, name)
+    ref = _run(dd, O, name, p, 2, dtype=dtype, profile=True)
+    assert any(k.startswith(kern) and k.endswith("|fwd_head") for k in ref["keys"]), ref["keys"]
+    monkeypatch.setenv("DDPG_FWD_PACK", "0")
+    got = _run(dd, O, name, p, 2, dtype=dtype, profile=True)
+    assert not any(k.endswith("|fwd_head") and "pack_kernel" in k for k in got["keys"]), got["keys"]
     _bitwise(got, ref)
 
 

@@ -16,7 +16,8 @@ v, r, cfg, kp = sys.argv[1:5]
 d = json.load(open("gpurun_out/eab_%s_%s_%s.json" % (cfg, v, r)))
 ks = ""
 if kp:
-    ks = " ".join("%s=%.2fus*%g" % (k.split("<")[0], x["avg_us"], x["per_step"])
+    # compact contract line: kernels as {name: [avg_us, per_step]}
+    ks = " ".join("%s=%.2fus*%g" % (k.split("<")[0], x[0], x[1])
                   for k, x in d["kernels"].items() if k.startswith(kp))
 print(v, r, d["value"], d["step_latency"]["median_ms"], d["roofline"]["kernel"],
       d["roofline"]["avg_launch_us"], d["roofline"]["frac"], ks, flush=True)
