@@ -427,6 +427,21 @@ DDPG_DEV void sb_actor_rows(const SbArgs& g, int r0, int valid, lds_f* red) {
   sb_save(g.sv.h1, g.sv.Bp, g.AH1, h1, r0);
   sb_save(g.sv.h2, g.sv.Bp, g.AH2, h2, r0);
   sb_save(g.sv.o, g.sv.Bp, g.A, o, r0);
+  if (g.A == 1) {
+    // one action (the reference's InvertedPendulum): dz3 is a per-row scalar,
+    // so the actor backward (networks.py:44) is dz3 times a per-row vector
+    // that needs no critic: v2 = W3 * elu'(h2), v1 = (v2 . W2^T) * elu'(h1)
+    // (W2^T from its row-major shadow).  Saved in dz2 / dz1's place; the
+    // actor's weight-gradient kernel scales them by phase 3's dz3.
+    lds_f* v2 = h2 + 4 * g.LW;
+    lds_f* v1 = v2 + 4 * g.LW;
+    for (int idx = tid; idx < 4 * g.AH2; idx += SB_NT)
+      v2[idx] = __fmul_rn(P[g.aW3 + (idx >> 2)], elu_grad_factor(h2[idx]));
+    __syncthreads();
+    sb_dense1(sb_op(v2, g.AH2, GLB(g.w2T), g.AH1, g.AH1, nullptr, SB_AUX, v1, h1), red);
+    sb_save(g.sv.dz2, g.sv.Bp, g.AH2, v2, r0);
+    sb_save(g.sv.dz1, g.sv.Bp, g.AH1, v1, r0);
+  }
 }
 
 // Phase 1's target workgroups: the TD target of the same rows (ddpg.py:90-97)
@@ -613,8 +628,10 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
       }
     };
     ld(xs, g.sv.xs, g.S, LX);
-    ld(h1, g.sv.h1, g.AH1, g.AH1);
-    ld(h2, g.sv.h2, g.AH2, g.AH2);
+    if (g.A != 1) {  // A == 1: phase 1 formed the actor backward per unit dz3
+      ld(h1, g.sv.h1, g.AH1, g.AH1);
+      ld(h2, g.sv.h2, g.AH2, g.AH2);
+    }
     for (int idx = tid; idx < 4 * LX; idx += SB_NT) {
       const int k = idx >> 2, r = idx & 3;
       const float v = (r < valid && k < g.A) ? g.sv.o[(size_t)k * Bp + r0 + r] : 0.f;
@@ -651,6 +668,11 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
     dz3[idx] = (idx & 3) < valid ? __fmul_rn(dy, __fsub_rn(1.f, __fmul_rn(ov, ov))) : 0.f;
   }
   __syncthreads();
+  if (g.A == 1) {
+    sb_save(g.sv.dz3, g.sv.Bp, g.A, dz3, r0);
+    SB_STAMP_SYNC(42);
+    return;
+  }
   // ---- actor backward (networks.py:44)
   // dz2 = dz3 . W3^T * elu'(h2) -> dh   (K = A is tiny: one thread per output)
   for (int idx = tid; idx < 4 * g.AH2; idx += SB_NT) {
@@ -731,7 +753,8 @@ constexpr int SB_GU = 16;  // float4s (4 batch rows each) per batch of loads
 // The critic's call forms dQ = -((1/B) * (2 * (y - q))) per row (the MSE
 // gradient, networks.py:136, from phase 1's saved q and TD target) into LDS
 // first; its tensors' saved output gradients are per unit dQ (sdq), scaled
-// by dQ[b] as they are read.  Its block 0 also forms the step stats: loss
+// by dQ[b] as they are read.  The actor's call at A == 1 does the same with
+// phase 3's dz3 (its dz1 / dz2 saved per unit dz3 by phase 1).  Its block 0 also forms the step stats: loss
 // partials and max Q per 4-row group in row order, then summed in group order.
 constexpr int SB_MAXB = 512;  // rows of the small path (sb_setup's sb_max_b)
 __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTab tab, int net,
@@ -743,6 +766,13 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
   __shared__ __attribute__((aligned(16))) float dqs[SB_MAXB];
   __shared__ float sp[2][SB_MAXB / SB_R];
   const bool crit = net == 1 && mode != 2;  // grid-uniform
+  // the actor's call at A == 1: its saved output gradients are per unit dz3
+  const bool act1 = net == 0 && mode != 2 && g.A == 1;
+  if (act1) {
+    for (int b = threadIdx.x; b < ((g.B + 3) & ~3); b += SB_GT)
+      dqs[b] = b < g.B ? g.sv.dz3[b] : 0.f;
+    __syncthreads();
+  }
   if (crit) {
     for (int b = threadIdx.x; b < ((g.B + 3) & ~3); b += SB_GT) {
       float dq = 0.f;
@@ -787,7 +817,7 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
   const f32x4* xp = T.X ? reinterpret_cast<const f32x4*>(T.X + (size_t)kc * T.ldx) : nullptr;
   const f32x4* dp = T.dY ? reinterpret_cast<const f32x4*>(T.dY + (size_t)nc * T.ldy) : nullptr;
   const lds_v4* dq4 = reinterpret_cast<const lds_v4*>(LDS(dqs));
-  const bool sdq = crit && T.sdq;
+  const bool sdq = (crit || act1) && T.sdq;
   const int nq = mode == 2 ? 0 : (g.B + 3) >> 2;
   float gv = mode == 2 ? g.grad[i] : 0.f;
   for (int q0 = 0; q0 < nq; q0 += SB_GU) {

@@ -1222,11 +1222,13 @@ void sb_setup(ddpg_ctx* c) {
     };
     SbGradTab& ta = c->sb_tab[0];  // actor (networks.py:39-47)
     ta.n = 0;
-    add(ta, L.a[AW1], sv.xs, sv.dz1);
-    add(ta, L.a[AB1], nullptr, sv.dz1);
-    add(ta, L.a[AW2], sv.h1, sv.dz2);
-    add(ta, L.a[AB2], nullptr, sv.dz2);
-    add(ta, L.a[AW3], sv.h2, sv.dz3);
+    // one action: dz1 / dz2 saved per unit dz3 (small_batch.h sb_actor_rows)
+    const int a1 = c->A == 1;
+    add(ta, L.a[AW1], sv.xs, sv.dz1, a1);
+    add(ta, L.a[AB1], nullptr, sv.dz1, a1);
+    add(ta, L.a[AW2], sv.h1, sv.dz2, a1);
+    add(ta, L.a[AB2], nullptr, sv.dz2, a1);
+    add(ta, L.a[AW3], sv.h2, a1 ? nullptr : sv.dz3, a1);
     close(ta);
     ta.shadow = 2;
     SbGradTab& tc = c->sb_tab[1];  // critic (networks.py:130-137)
