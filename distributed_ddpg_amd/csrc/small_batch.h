@@ -737,12 +737,17 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
 // sum over b per element, no partial slabs), TF ApplyAdam with this step's
 // alpha, soft update of the target, and the transposed shadow of the dX
 // weight.  net: 0 actor, 1 critic; the critic call also finalises the step
-// stats.  Thread (k, n) reads column k of X and column n of dY straight from
-// global memory, SB_GU rows per batch with every load of a batch issued before
-// the first FMA (a wave shares k, so its X loads are one line and its dY
-// loads one contiguous run); the Adam state is loaded first so that its
-// round trip overlaps the gradient's.
-constexpr int SB_GU = 16;  // float4s (4 batch rows each) per batch of loads
+// stats.  A block owns a TK x TN tile of one tensor; its X and dY rows are
+// staged through LDS 64 batch rows at a time by coalesced loads (round 6:
+// before, every lane streamed its own dY row from global memory, 64 lines
+// per load instruction), and thread (k, n) sums its products over b in
+// order from LDS; the Adam state is loaded first so that its round trip
+// overlaps the gradient's.
+constexpr int SB_GC = 64;  // batch rows per staged chunk (16 float4s per tile row)
+constexpr int SB_GLD = SB_GC + 4;  // LDS row stride (floats): lanes on different rows
+                                   // read 16-B slots 4 banks apart, conflict-free
+constexpr int SB_GROWS = SB_GT + 1;  // tile rows TK + TN <= 257 (TK * TN = SB_GT, TN <= 64)
+constexpr int SB_GSJ = (SB_GROWS * 16 + SB_GT - 1) / SB_GT;  // staged float4s per thread
 // mode 0: gradient + Adam + soft update (+ stats), one launch.  A step with
 // a communicator (data parallelism at small batches) splits it around the
 // RCCL sum of the gradient buffer: mode 1 computes and stores this rank's
@@ -763,37 +768,11 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
   const int sbase = net == 1 ? 48 : 56;
 #endif
   SB_STAMP(sbase);
-  __shared__ __attribute__((aligned(16))) float dqs[SB_MAXB];
   __shared__ float sp[2][SB_MAXB / SB_R];
+  __shared__ __attribute__((aligned(16))) float stg[SB_GROWS * SB_GLD];
   const bool crit = net == 1 && mode != 2;  // grid-uniform
   // the actor's call at A == 1: its saved output gradients are per unit dz3
   const bool act1 = net == 0 && mode != 2 && g.A == 1;
-  if (act1) {
-    for (int b = threadIdx.x; b < ((g.B + 3) & ~3); b += SB_GT)
-      dqs[b] = b < g.B ? g.sv.dz3[b] : 0.f;
-    __syncthreads();
-  }
-  if (crit) {
-    for (int b = threadIdx.x; b < ((g.B + 3) & ~3); b += SB_GT) {
-      float dq = 0.f;
-      if (b < g.B) dq = -__fmul_rn(g.inv_b, __fmul_rn(2.f, __fsub_rn(g.sv.y[b], g.sv.q[b])));
-      dqs[b] = dq;
-    }
-    if (blockIdx.x == 0) {
-      for (int w = threadIdx.x; w < nslab; w += SB_GT) {
-        float lsum = 0.f, qmax = -INFINITY;
-        for (int r = 0; r < SB_R && w * SB_R + r < g.B; ++r) {
-          const float q = g.sv.q[w * SB_R + r];
-          const float d = __fsub_rn(g.sv.y[w * SB_R + r], q);
-          lsum += __fmul_rn(d, d);
-          qmax = fmaxf(qmax, q);
-        }
-        sp[0][w] = lsum;
-        sp[1][w] = qmax;
-      }
-    }
-    __syncthreads();
-  }
   int ti = 0;
 #pragma unroll
   for (int i = 1; i < SB_MAXT; ++i)
@@ -814,33 +793,86 @@ __global__ __launch_bounds__(SB_GT) void sb_wgrad_adam_kernel(SbArgs g, SbGradTa
     p0 = g.theta[i];
     t0 = g.target[i];
   }
-  const f32x4* xp = T.X ? reinterpret_cast<const f32x4*>(T.X + (size_t)kc * T.ldx) : nullptr;
-  const f32x4* dp = T.dY ? reinterpret_cast<const f32x4*>(T.dY + (size_t)nc * T.ldy) : nullptr;
-  const lds_v4* dq4 = reinterpret_cast<const lds_v4*>(LDS(dqs));
+  // X rows [k0, k0 + TK) and dY rows [n0, n0 + TN) of the tile, SB_GC batch
+  // rows at a time, staged into LDS by coalesced 16-B loads (the dQ / dz3
+  // scaling applied there), then each thread's ordered sum over b from LDS
+  const int k0 = (local / ntn) * T.TK, n0 = (local % ntn) * T.TN;
+  const int rows = T.TK + T.TN;
   const bool sdq = (crit || act1) && T.sdq;
-  const int nq = mode == 2 ? 0 : (g.B + 3) >> 2;
+  const int nB = mode == 2 ? 0 : g.B;
+  lds_f* const st = LDS(stg);
   float gv = mode == 2 ? g.grad[i] : 0.f;
-  for (int q0 = 0; q0 < nq; q0 += SB_GU) {
-    f32x4 xv[SB_GU], dv[SB_GU];
-#pragma unroll
-    for (int u = 0; u < SB_GU; ++u) {
-      const int qq = min(q0 + u, nq - 1);
-      xv[u] = xp ? xp[qq] : f32x4{1.f, 1.f, 1.f, 1.f};
-      dv[u] = dp ? dp[qq] : f32x4{1.f, 1.f, 1.f, 1.f};
-    }
-    if (sdq) {
-#pragma unroll
-      for (int u = 0; u < SB_GU; ++u) {
-        const f32x4 d = dq4[min(q0 + u, nq - 1)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dv[u][e] = __fmul_rn(d[e], dv[u][e]);
+  for (int b0 = 0; b0 < nB; b0 += SB_GC) {
+    const int nq4 = (min(SB_GC, nB - b0) + 3) >> 2;  // float4s per staged row
+    // a thread stages quad qd of every row it touches (SB_GT is a multiple
+    // of 16): its rows' per-row scale comes from one float4 of the saves,
+    // loaded with the tile in the same round trip
+    const int qd = tid & 15, bq = b0 + 4 * qd;
+    f32x4 sa = f32x4{0.f, 0.f, 0.f, 0.f}, sb = sa;
+    if ((crit || act1) && qd < nq4) {
+      if (crit) {
+        sa = *reinterpret_cast<const f32x4*>(g.sv.y + bq);
+        sb = *reinterpret_cast<const f32x4*>(g.sv.q + bq);
+      } else {
+        sa = *reinterpret_cast<const f32x4*>(g.sv.dz3 + bq);
       }
     }
+    f32x4 v[SB_GSJ];
 #pragma unroll
-    for (int u = 0; u < SB_GU; ++u)
+    for (int j = 0; j < SB_GSJ; ++j) {  // every load in flight before the stores
+      const int f = tid + SB_GT * j, r = f >> 4, q = f & 15;
+      v[j] = f32x4{1.f, 1.f, 1.f, 1.f};
+      if (r < rows && q < nq4) {
+        const float* src = nullptr;
+        if (r < T.TK)
+          src = T.X ? T.X + (size_t)min(k0 + r, T.K - 1) * T.ldx : nullptr;
+        else
+          src = T.dY ? T.dY + (size_t)min(n0 + r - T.TK, T.N - 1) * T.ldy : nullptr;
+        if (src) v[j] = *reinterpret_cast<const f32x4*>(src + b0 + 4 * q);
+      }
+    }
+    // dQ = -((1/B) * (2 * (y - q))) (critic; networks.py:136) or dz3
+    // (actor, A == 1) per row, 0 past B
+    f32x4 d;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      d[e] = bq + e >= nB ? 0.f
+             : crit       ? -__fmul_rn(g.inv_b, __fmul_rn(2.f, __fsub_rn(sa[e], sb[e])))
+                          : sa[e];
+    if (crit && blockIdx.x == 0 && tid < 16 && qd < nq4) {
+      // step stats of row group bq / 4: loss partial and max Q, in row order
+      float lsum = 0.f, qmax = -INFINITY;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        gv = (4 * (q0 + u) + e < g.B) ? fmaf(xv[u][e], dv[u][e], gv) : gv;
+        if (bq + e < nB) {
+          const float dd = __fsub_rn(sa[e], sb[e]);
+          lsum += __fmul_rn(dd, dd);
+          qmax = fmaxf(qmax, sb[e]);
+        }
+      sp[0][bq >> 2] = lsum;
+      sp[1][bq >> 2] = qmax;
+    }
+#pragma unroll
+    for (int j = 0; j < SB_GSJ; ++j) {
+      const int f = tid + SB_GT * j, r = f >> 4;
+      if (r < rows && qd < nq4) {
+        f32x4 w = v[j];
+        if (sdq && r >= T.TK) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = __fmul_rn(d[e], w[e]);
+        }
+        *reinterpret_cast<lds_v4*>(st + r * SB_GLD + 4 * qd) = w;
+      }
+    }
+    __syncthreads();
+    const lds_v4* xr = reinterpret_cast<const lds_v4*>(st + kl * SB_GLD);
+    const lds_v4* dr = reinterpret_cast<const lds_v4*>(st + (T.TK + nl) * SB_GLD);
+    for (int q = 0; q < nq4; ++q) {
+      const f32x4 xv = xr[q], dv = dr[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gv = (b0 + 4 * q + e < nB) ? fmaf(xv[e], dv[e], gv) : gv;
+    }
+    __syncthreads();  // the next chunk's stores reuse the tile
   }
   SB_STAMP(sbase + 1);
   if (ok && mode == 1) g.grad[i] = gv;
