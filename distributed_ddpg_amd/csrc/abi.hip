@@ -171,6 +171,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.tk_fwd = !env_is("DDPG_TK_FWD", "0");
       c->sw.gemm_pack = !env_is("DDPG_GEMM_PACK", "0");
       c->sw.fwd_pack = !env_is("DDPG_FWD_PACK", "0");
+      c->sw.gather16 = !env_is("DDPG_GATHER16", "0");
       c->sw.half_twin = !env_is("DDPG_HALF_TWIN", "0");
       c->sw.skinny_nl = !env_is("DDPG_SKINNY_NL", "0");
       c->sw.prof_shapes = env_is("DDPG_PROF_SHAPES", "1");

@@ -288,6 +288,7 @@ struct ddpg_ctx {
     bool half_twin = true;   // DDPG_HALF_TWIN=0: bf16 config stores cat2 / dcat state halves in fp32 too
     bool gemm_pack = true;   // DDPG_GEMM_PACK=0: deferred GEMMs launched one by one
     bool fwd_pack = true;    // DDPG_FWD_PACK=0: the step's forward layers in sequence
+    bool gather16 = true;    // DDPG_GATHER16=0: the one-row-per-wave gather everywhere
     bool tk_fwd = true;      // DDPG_TK_FWD=0: thin_k's generic epilogue for forward parts too
     int kc_splits = 4;       // DDPG_KCOMB_SPLITS=s: at most s splits per tile (2 .. KC_MAXS)
     bool kc_wgrad = true;    // DDPG_KCOMB_WGRAD=0: data-parallel weight gradients keep their slabs

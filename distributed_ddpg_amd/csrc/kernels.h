@@ -81,6 +81,73 @@ __global__ void gather_rows_kernel(const int* __restrict__ slots, int B,
   }
 }
 
+// The same for an fp32 ring with 4-aligned S <= 64 * QI and A <= 64, 16 rows
+// per block: the rows' slots (in pinned host memory when read in place) come
+// in one coalesced read by 16 lanes and are parked in LDS -- one host read per
+// 16 rows instead of one per row -- and each wave copies 4 rows at once (lane:
+// row lane >> 4, feature quads lane & 15 + 16 u), every load of its 4 rows in
+// flight together.  Same values as gather_rows_kernel.
+template <int QI>
+__global__ __launch_bounds__(256) void gather_rows16_kernel(
+    const int* __restrict__ slots, int B, const float* __restrict__ rs,
+    const float* __restrict__ ra, const float* __restrict__ rr, const float* __restrict__ rt,
+    const float* __restrict__ rs2, int S, int A, float* __restrict__ s, float* __restrict__ s2,
+    int lds, float* __restrict__ a, int lda, float* __restrict__ r, float* __restrict__ t,
+    const double* __restrict__ mean, const double* __restrict__ scale, __bf16* __restrict__ sh,
+    __bf16* __restrict__ s2h, long long hps, int hnp) {
+  __shared__ int sl[16];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int b0 = blockIdx.x * 16;
+  if (tid < 16) sl[tid] = b0 + tid < B ? slots[b0 + tid] : 0;
+  __syncthreads();
+  const int i = 4 * wave + (lane >> 4), q = lane & 15, b = b0 + i;
+  if (b >= B) return;
+  const size_t slot = (size_t)sl[i];
+  float4 x[QI], x2[QI];
+#pragma unroll
+  for (int u = 0; u < QI; ++u) {
+    const int j = 4 * (q + 16 * u);
+    x[u] = x2[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < S) {
+      x[u] = *reinterpret_cast<const float4*>(rs + slot * S + j);
+      x2[u] = *reinterpret_cast<const float4*>(rs2 + slot * S + j);
+    }
+  }
+  float av[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) av[u] = q + 16 * u < A ? ra[slot * A + q + 16 * u] : 0.f;
+  float rv = 0.f, tv = 0.f;
+  if (q == 0) {
+    rv = rr[slot];
+    tv = rt[slot];
+  }
+#pragma unroll
+  for (int u = 0; u < QI; ++u) {
+    const int j = 4 * (q + 16 * u);
+    if (j >= S) continue;
+    if (mean) {
+      float* px = &x[u].x;
+      float* px2 = &x2[u].x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        px[e] = (float)(((double)px[e] - mean[j + e]) / scale[j + e]);
+        px2[e] = (float)(((double)px2[e] - mean[j + e]) / scale[j + e]);
+      }
+    }
+    *reinterpret_cast<float4*>(s + (size_t)b * lds + j) = x[u];
+    *reinterpret_cast<float4*>(s2 + (size_t)b * lds + j) = x2[u];
+    if (sh) store_twin4(sh + (size_t)b * lds + j, hps, hnp, x[u]);
+    if (s2h) store_twin4(s2h + (size_t)b * lds + j, hps, hnp, x2[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (q + 16 * u < A) a[(size_t)b * lda + q + 16 * u] = av[u];
+  if (q == 0) {
+    r[b] = rv;
+    t[b] = tv;
+  }
+}
+
 // ---------------------------------------------------------------- thin heads
 // actor output: o = tanh(sum_t part[t][b][a]); mu = o * scale  (networks.py:59-61)
 // Sum of NT strided slab values in slab order (z = ((v0 + v1) + v2) + ...),

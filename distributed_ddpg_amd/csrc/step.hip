@@ -1368,6 +1368,18 @@ int ddpg_soft_update(ddpg_ctx* c, int mask) {
 // ---------------------------------------------------------------- fused step
 static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
   ProfScope ps(c, "gather", 0, (double)B * (2.0 * c->S + c->A + 2) * 8.0);
+  const Twin ts = act_twin(c, c->s), ts2 = act_twin(c, c->s2);
+  if (c->sw.gather16 && !rb->rsd && c->S % 4 == 0 && c->S <= 512 && c->A <= 64 &&
+      c->ldS % 4 == 0 && (ts.ps & 3) == 0 && (ts2.ps & 3) == 0) {
+    auto k = c->S <= 64 ? gather_rows16_kernel<1> : gather_rows16_kernel<8>;
+    hipLaunchKernelGGL(k, dim3(ceil_div(B, 16)), dim3(256), 0, c->cur,
+                       c->slots_src ? c->slots_src : c->d_slots, B, rb->rs, rb->ra, rb->rr,
+                       rb->rt, rb->rs2, c->S, c->A, c->s, c->s2, c->ldS, c->a, c->ldA, c->r,
+                       c->t, c->has_scaler ? c->dmean : nullptr,
+                       c->has_scaler ? c->dscale : nullptr, ts.p, ts2.p, ts.ps, c->hnp);
+    HIP_TRY(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, c->cur,
                      c->slots_src ? c->slots_src : c->d_slots, B, rb->rs, rb->ra, rb->rr, rb->rt,
                      rb->rs2, rb->rsd, rb->rs2d,

@@ -66,7 +66,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
             "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW",
-            "DDPG_FWD_PACK")
+            "DDPG_FWD_PACK", "DDPG_GATHER16")
 
 
 @pytest.fixture(scope="module")
@@ -157,6 +157,8 @@ def _oracle(O, name, p, rows, steps):
     ("DDPG_SKINNY_NL", "0", "wide"),
     ("DDPG_SLOTS_H2D", "1", "wide"),
     ("DDPG_SLOTS_H2D", "1", "ip"),
+    ("DDPG_GATHER16", "0", "wide"),
+    ("DDPG_GATHER16", "0", "wides"),
 ])
 def test_placement_switch_bitwise(dd, O, monkeypatch, switch, value, name):
     _clear(monkeypatch)
