@@ -708,6 +708,11 @@ def main():
     if world != args.gpus:
         log("[bench] note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     import torch
+    if os.environ.get("DDPG_BENCH_ONE_DEVICE") == "1":
+        # rehearsal of an N-rank run on a one-GPU box (every rank on device 0,
+        # with DDPG_LIB_PATH=tools/shm/libddpg_shm.so standing in for RCCL,
+        # which refuses two ranks on one device; tools/gpu/r6_rehearse.sh)
+        local = 0
     if local >= torch.cuda.device_count():
         raise SystemExit("[bench] rank %d: LOCAL_RANK %d but only %d GPU(s) visible"
                          % (rank, local, torch.cuda.device_count()))
@@ -715,7 +720,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with stdout_to_stderr():   # Gloo prints its peer-connection line on fd 1
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     cfg = args.config
     dtype = args.dtype or DEFAULT_DTYPE[cfg]

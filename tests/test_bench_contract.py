@@ -65,3 +65,36 @@ def test_contract_line_world_gt_1_shape():
     c = bench.compact_line(full)
     assert len(json.dumps(c)) <= bench.CONTRACT_LINE_MAX
     assert c["cpu_baseline"] is None and c["exchange"] == full["exchange"]
+
+
+_GLOO_CHILD = r"""
+import os, sys
+sys.path.insert(0, %r)
+import bench
+import torch.distributed as dist
+with bench.stdout_to_stderr():
+    dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=2)
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_gloo_init_keeps_stdout_clean(tmp_path):
+    """bench.py's N > 1 ranks init their gloo group inside stdout_to_stderr:
+    Gloo prints a peer-connection line on fd 1 at init, which would put a
+    second line beside the contract's one JSON line (found rehearsing the
+    N-rank bench on one GPU, tools/gpu/r6_rehearse.sh)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "child.py"
+    src.write_text(_GLOO_CHILD % root)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT="29671")
+        procs.append(subprocess.Popen([sys.executable, str(src)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, cwd=root))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert [p.returncode for p in procs] == [0, 0], [o[1][-500:] for o in outs]
+    assert all(o[0] == b"" for o in outs), [o[0][:200] for o in outs]
