@@ -153,6 +153,60 @@ def test_mountaincar_scaler_parity(dd, O, widths):
     sess.close()
 
 
+# ---------------------------------------------------------------- ragged shapes
+@pytest.mark.parametrize("S,A,H1,H2,B,steps", [(17, 6, 400, 300, 600, 3),
+                                               (64, 16, 1024, 1024, 4100, 2)])
+def test_large_path_ragged_shapes(dd, O, S, A, H1, H2, B, steps):
+    """The large-batch path on shapes that fill no tile.  (a) B = 600 (past
+    the small path's 512, not a multiple of 64 or 128), S = 17 (thin_k's K
+    padded to 24), A = 6, and the reference's 400 / 300 widths
+    (parameters.py; 400 and 300 are not multiples of 128, and the concat
+    2 x 400 not of 256): every GEMM has partial row and column tiles.  (b) the
+    C3 widths at B = 4100, four rows past the headline batch: a partial last
+    row tile on every batch-row GEMM and a ragged last K-split of every weight
+    gradient.  Fused steps against the float64 oracle on the same sampled
+    rows, with the fused-step bars of test_gpu_parity (fp32 restatement drift
+    as the floor)."""
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner, Profile
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    from test_gpu_parity import assert_steps_close
+    scale = 2.0
+    rng = np.random.default_rng(61)
+    p = _noisy_params(O, S, A, H1, H2, seed=70)
+    sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B)
+    n = max(3000, 2 * B)
+    rb = ReplayBuffer(n + 1000, 1234)
+    rows = _rows(rng, n, S, A, scale)
+    rb.add_batch(*rows)
+    fl = FusedLearner(sess, rb, B)
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    L32 = O.Learner(S, A, H1, H2, scale, dtype=np.float32, params=p, init_blend=False)
+    prof = Profile(sess)
+    prof.enable(True)
+    ref_rng = random.Random(1234)
+    for _ in range(steps):
+        idx = np.array(ref_rng.sample(range(n), B))
+        qmax, loss = fl.step(stats=True)
+        s, a, r, t, s2 = (x[idx] for x in rows)
+        out = L.step(s, a, r, t, s2)
+        L32.step(s, a, r, t, s2)
+        assert abs(loss - float(out["loss"])) <= GRAD_TOL * abs(float(out["loss"]))
+        q_ref = float(np.max(out["q"]))
+        assert abs(qmax - q_ref) <= FWD_TOL * max(1.0, abs(q_ref)) * 10
+    keys = sorted(prof.read())
+    prof.enable(False)
+    assert not any(k.startswith("sb_") for k in keys), keys  # the large-batch path ran
+    assert any(k.startswith("gemm_") for k in keys), keys
+    for which, net, keys_ in ((_lib.ACTOR, "actor", O.ACTOR_KEYS),
+                              (_lib.CRITIC, "critic", O.CRITIC_KEYS),
+                              (_lib.ACTOR_TARGET, "actor_t", O.ACTOR_KEYS),
+                              (_lib.CRITIC_TARGET, "critic_t", O.CRITIC_KEYS)):
+        for k, v in zip(keys_, sess.get_params(which)):
+            assert_steps_close(v, L.state()[net][k], L32.state()[net][k], (net, k))
+    sess.close()
+
+
 # ---------------------------------------------------------------- C3
 def test_c3_gradients_and_adam_slots(dd, O):
     """B=4096, 1024/1024 (the headline shape): after one fused step the
