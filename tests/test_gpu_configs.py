@@ -382,3 +382,39 @@ def test_c5_bf16_full_dims(dd, O):
             bad = big & (np.abs(step + lr * np.sign(g)) > tol)
             assert not bad.any(), (net, k, int(bad.sum()), int(big.sum()))
     sess.close()
+
+
+def test_bf16_ragged_shapes(dd, O):
+    """The bf16 configuration on shapes that fill no tile: S = 100 (first
+    layers on the GEMMs, K not a multiple of the 64-deep step), A = 7, widths
+    600 / 520 (not multiples of 128 or 256), B = 1000 (not a multiple of the
+    256-row tile).  One fused step against the float64 oracle at the stated
+    bf16 bars of test_c5_bf16_full_dims: loss, gradients norm-wise and max-rel
+    per tensor, every parameter within two Adam steps."""
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B = 100, 7, 600, 520, 1.0, 1000
+    p = _noisy_params(O, S, A, H1, H2, seed=80, amp=0.02)
+    sess, actor, critic = _open(dd, O, S, A, H1, H2, scale, p, batch_max=B, dtype="bf16")
+    rng = np.random.default_rng(81)
+    rows = _rows(rng, 3000, S, A, scale)
+    rb = ReplayBuffer(4000, 1234)
+    rb.add_batch(*rows)
+    fl = FusedLearner(sess, rb, B)
+    qmax, loss = fl.step(stats=True)
+    idx = np.array(random.Random(1234).sample(range(3000), B))
+    L = O.Learner(S, A, H1, H2, scale, dtype=np.float64, params=p, init_blend=False)
+    out = L.step(*(x[idx] for x in rows))
+    assert abs(loss - float(out["loss"])) <= 2e-2 * abs(float(out["loss"]))
+    for gw, ref, keys_ in ((_lib.CRITIC_GRAD, out["critic_grads"], O.CRITIC_KEYS),
+                           (_lib.ACTOR_GRAD, out["actor_grads"], O.ACTOR_KEYS)):
+        for k, g in zip(keys_, sess.get_params(gw)):
+            assert normrel(g, ref[k]) < BF16_GRAD_NORM_TOL, ("grad", k, normrel(g, ref[k]))
+            assert maxrel(g, ref[k]) < BF16_GRAD_MAXREL, ("grad max-rel", k, maxrel(g, ref[k]))
+    for which, net, names, lr in ((_lib.ACTOR, "actor", O.ACTOR_KEYS, 1e-4),
+                                  (_lib.CRITIC, "critic", O.CRITIC_KEYS, 1e-3)):
+        for k, v in zip(names, sess.get_params(which)):
+            r = L.state()[net][k].reshape(v.shape)
+            assert np.max(np.abs(v - r)) <= 2.02 * lr, (net, k, np.max(np.abs(v - r)))
+    sess.close()
