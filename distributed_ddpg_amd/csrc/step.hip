@@ -1390,14 +1390,22 @@ static void gather_launch(ddpg_ctx* c, ddpg_replay* rb, int B) {
   HIP_TRY(hipGetLastError());
 }
 
-static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg,
-                        ddpg_stats* stats) {
+// Every argument check of a fused step, before anything has a side effect: a
+// rejected call leaves the replay's sampler, the parameters and the Adam
+// state as they were.
+static void check_step(ddpg_ctx* c, const ddpg_replay* rb, int Bg, bool sampled) {
   if (rb->S != c->S || rb->A != c->A)
     throw einval("replay dims (S=%d, A=%d) != network dims (S=%d, A=%d)", rb->S, rb->A, c->S,
                  c->A);
-  if (Bg % c->world) throw einval("global batch %d not divisible by world %d", Bg, c->world);
+  if (Bg <= 0 || Bg % c->world) throw einval("global batch %d not divisible by world %d", Bg, c->world);
+  check_b(c, Bg / c->world);
+  if (sampled && rb->count < Bg)  // random.sample without replacement
+    throw einval("replay holds %lld rows < batch %d", (long long)rb->count, Bg);
+}
+
+static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg,
+                        ddpg_stats* stats) {
   const int B = Bg / c->world;
-  check_b(c, B);
   const int64_t* mine = idx + (size_t)c->rank * B;  // this rank's slice of the global draw
   const float inv_b = 1.0f / (float)Bg;
   const bool small = takes_small(c, B);
@@ -1525,7 +1533,7 @@ int ddpg_learner_step(ddpg_ctx* c, ddpg_replay* rb, int Bg, ddpg_stats* stats) {
   return guard(c, [&] {
     if (!rb) throw einval("null replay");
     replay_flush(rb);
-    if (rb->count < Bg) throw einval("replay holds %lld rows < batch %d", (long long)rb->count, Bg);
+    check_step(c, rb, Bg, true);
     c->idx_tmp.resize(Bg);
     if (rb->sampler.sample(rb->count, Bg, c->idx_tmp.data()) != 0) throw einval("sample failed");
     step_common(c, rb, c->idx_tmp.data(), Bg, stats);
@@ -1537,6 +1545,7 @@ int ddpg_learner_step_indices(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, 
   return guard(c, [&] {
     if (!rb || !idx) throw einval("null argument");
     replay_flush(rb);
+    check_step(c, rb, Bg, false);
     for (int i = 0; i < Bg; ++i)
       if (idx[i] < 0 || idx[i] >= rb->count) throw einval("index %lld out of range", (long long)idx[i]);
     step_common(c, rb, idx, Bg, stats);

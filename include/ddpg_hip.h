@@ -196,7 +196,10 @@ int ddpg_replay_sample_batch_f64(ddpg_replay* rb, int B, double* s, float* a, do
  * this rank processes rows [rank*B/world, (rank+1)*B/world) and gradients
  * are summed over ranks with RCCL; with a communicator the stats are the
  * global-batch ones (max over ranks of max(Q), sum of the loss shares).
- * stats may be NULL (no host sync). */
+ * stats may be NULL (no host sync).  Argument errors (replay dims, B outside
+ * [1, batch_max] per rank or not divisible by world, fewer than B rows) return
+ * a negative status BEFORE anything moves: the sampler, parameters and Adam
+ * state are as they were. */
 int ddpg_learner_step(ddpg_ctx* ctx, ddpg_replay* rb, int B, ddpg_stats* stats);
 /* Same, with an explicit host index list (deque positions, length B). */
 int ddpg_learner_step_indices(ddpg_ctx* ctx, ddpg_replay* rb, const int64_t* idx, int B,

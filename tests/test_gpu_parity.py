@@ -340,6 +340,60 @@ def test_fused_learner_step_parity(dd, O, name):
     sess.close()
 
 
+def _fused_state(sess):
+    from distributed_ddpg_amd import _lib
+    return [sess.get_params(w) for w in (_lib.ACTOR, _lib.CRITIC, _lib.ACTOR_TARGET,
+                                         _lib.CRITIC_TARGET, _lib.ACTOR_ADAM_M,
+                                         _lib.ACTOR_ADAM_V, _lib.CRITIC_ADAM_M,
+                                         _lib.CRITIC_ADAM_V)]
+
+
+@pytest.mark.parametrize("name", ["ip", "wide"])
+def test_rejected_calls_leave_state_unchanged(dd, O, name):
+    """Error behaviour of the fused step (the reference's feed would raise TF's
+    InvalidArgumentError): a batch past batch_max, a replay of other dims, a
+    replay holding fewer rows than the batch, a parameter upload of the wrong
+    size and a wrong parameter-set id each raise DDPGError, and none of them
+    moves anything -- the replay's sampler, the parameters, the Adam state:
+    the session's next two steps equal, bit for bit, those of a session that
+    never saw the rejected calls (small path "ip", GEMM path "wide")."""
+    from distributed_ddpg_amd import _lib
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    runs = []
+    for bad in (False, True):
+        sess, actor, critic = _session(dd, O, name, p, batch_max=B)
+        rb = ReplayBuffer(5000, 1234)
+        _fill(rb, S, A, 3000, scale, seed=2)
+        if bad:
+            with pytest.raises(_lib.DDPGError, match="batch"):
+                FusedLearner(sess, rb, B + 1).step()
+            other = ReplayBuffer(500, 99)
+            _fill(other, S + 1, A, 400, scale, seed=3)
+            with pytest.raises(_lib.DDPGError, match="replay dims"):
+                FusedLearner(sess, other, B).step()
+            few = ReplayBuffer(500, 7)
+            _fill(few, S, A, B - 1, scale, seed=4)
+            with pytest.raises(_lib.DDPGError, match="rows < batch"):
+                FusedLearner(sess, few, B).step()
+            w = sess.get_params(_lib.ACTOR)
+            with pytest.raises(_lib.DDPGError):
+                sess.set_params(_lib.ACTOR, w[:-1])
+            with pytest.raises(_lib.DDPGError):
+                sess.set_params(99, w)
+        fl = FusedLearner(sess, rb, B)
+        st = [fl.step(stats=True) for _ in range(2)]
+        runs.append((st, _fused_state(sess), fl.read_stats()))
+        sess.close()
+    (st0, s0, a0), (st1, s1, a1) = runs
+    assert st0 == st1 and a0 == a1
+    for x, y in zip(s0, s1):
+        for u, v in zip(x, y):
+            assert np.array_equal(u, v)
+
+
 def test_batch_4096_wide_step_properties(dd, O):
     """Full C3 shape (S=64, A=16, 1024/1024, B=4096): one fused step equals
     the oracle step on the same rows (fp64 oracle at full size)."""
