@@ -167,15 +167,22 @@ class Session:
     def sync(self):
         check(lib.ddpg_sync(self.ctx), self.ctx)
 
-    def _rows(self, x, cols):
+    def _rows(self, x, cols, any_batch=False):
+        """[B, cols] fp32 rows.  Training calls (batch statistics) need
+        1 <= B <= batch_max; forward-only calls (any_batch) take any B, as a
+        TF feed does -- their rows are independent, so a batch past
+        batch_max runs in batch_max-row pieces and B = 0 returns empty."""
         a = f32(x)
         if a.ndim == 1:
             a = a.reshape(-1, cols)
         if a.ndim != 2 or a.shape[1] != cols:
             raise ValueError("expected [B, %d] input, got %s" % (cols, a.shape))
-        if a.shape[0] > self.batch_max or a.shape[0] == 0:
+        if not any_batch and (a.shape[0] > self.batch_max or a.shape[0] == 0):
             raise ValueError("batch %d outside [1, %d]" % (a.shape[0], self.batch_max))
         return a
+
+    def _pieces(self, B):
+        return [(i, min(B, i + self.batch_max)) for i in range(0, B, self.batch_max)]
 
 
 def _transform(scaler, x):
@@ -214,9 +221,12 @@ class ActorNetwork:
 
     def _forward(self, inputs, target):
         ss = self.sess
-        s = ss._rows(self.preprocess_input(inputs), self.s_dim)
+        s = ss._rows(self.preprocess_input(inputs), self.s_dim, any_batch=True)
         out = np.empty((s.shape[0], self.a_dim), np.float32)
-        check(lib.ddpg_actor_forward(ss.ctx, int(target), fptr(s), s.shape[0], fptr(out)), ss.ctx)
+        for i, j in ss._pieces(s.shape[0]):
+            sp, op = np.ascontiguousarray(s[i:j]), np.empty((j - i, self.a_dim), np.float32)
+            check(lib.ddpg_actor_forward(ss.ctx, int(target), fptr(sp), j - i, fptr(op)), ss.ctx)
+            out[i:j] = op
         return out
 
     def predict(self, inputs):
@@ -279,11 +289,16 @@ class CriticNetwork:
 
     def _forward(self, inputs, action, target):
         ss = self.sess
-        s = ss._rows(self.preprocess_input(inputs), self.s_dim)
+        s = ss._rows(self.preprocess_input(inputs), self.s_dim, any_batch=True)
         B = s.shape[0]
         a = f32(action).reshape(B, self.a_dim)
         q = np.empty((B, 1), np.float32)
-        check(lib.ddpg_critic_forward(ss.ctx, int(target), fptr(s), fptr(a), B, fptr(q)), ss.ctx)
+        for i, j in ss._pieces(B):
+            sp, ap = np.ascontiguousarray(s[i:j]), np.ascontiguousarray(a[i:j])
+            qp = np.empty((j - i, 1), np.float32)
+            check(lib.ddpg_critic_forward(ss.ctx, int(target), fptr(sp), fptr(ap), j - i, fptr(qp)),
+                  ss.ctx)
+            q[i:j] = qp
         return q
 
     def predict(self, inputs, action):
@@ -295,11 +310,15 @@ class CriticNetwork:
     def action_gradients(self, inputs, actions):
         """networks.py:189-193: list of one [B, A] array (grad_ys = 1)."""
         ss = self.sess
-        s = ss._rows(self.preprocess_input(inputs), self.s_dim)
+        s = ss._rows(self.preprocess_input(inputs), self.s_dim, any_batch=True)
         B = s.shape[0]
         a = f32(actions).reshape(B, self.a_dim)
         da = np.empty((B, self.a_dim), np.float32)
-        check(lib.ddpg_critic_action_grad(ss.ctx, fptr(s), fptr(a), B, fptr(da)), ss.ctx)
+        for i, j in ss._pieces(B):  # grad_ys = 1 per row: rows independent
+            sp, ap = np.ascontiguousarray(s[i:j]), np.ascontiguousarray(a[i:j])
+            dp = np.empty((j - i, self.a_dim), np.float32)
+            check(lib.ddpg_critic_action_grad(ss.ctx, fptr(sp), fptr(ap), j - i, fptr(dp)), ss.ctx)
+            da[i:j] = dp
         return [da]
 
     def update_target_network(self):

@@ -159,6 +159,46 @@ def test_forward_parity(dd, O, name):
     sess.close()
 
 
+@pytest.mark.parametrize("name", ["ip", "wide"])
+def test_forward_methods_any_batch(dd, O, name):
+    """Forward-only methods take any batch, as a TF feed does: B = 0 returns
+    empty [0, A] / [0, 1] arrays, and a batch past the session's batch_max
+    runs in batch_max-row pieces -- within the forward bar of the oracle, and
+    equal, row for row, to the same rows asked for in one call of their own
+    size.  Training calls keep 1 <= B <= batch_max (their batch statistics
+    cannot be split): B = 0 and B = batch_max + 1 raise ValueError."""
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    sess, actor, critic = _session(dd, O, name, p, batch_max=B)
+    s, a, _ = _batch(name, seed=5, B=2 * B + 37)
+    assert actor.predict(s[:0]).shape == (0, A)
+    assert actor.predict_target(s[:0]).shape == (0, A)
+    assert critic.predict(s[:0], a[:0]).shape == (0, 1)
+    assert critic.action_gradients(s[:0], a[:0])[0].shape == (0, A)
+    s64, a64 = s.astype(np.float64), a.astype(np.float64)
+    mu = actor.predict(s)
+    assert mu.shape == (2 * B + 37, A)
+    assert rel(mu, O.actor_forward(f64(p["actor"]), s64, scale)[3]) < FWD_TOL
+    mut = actor.predict_target(s)
+    assert rel(mut, O.actor_forward(f64(p["actor_t"]), s64, scale)[3]) < FWD_TOL
+    q = critic.predict(s, a)
+    assert rel(q, O.critic_forward(f64(p["critic"]), s64, a64)[3]) < FWD_TOL
+    qt = critic.predict_target(s, a)
+    assert rel(qt, O.critic_forward(f64(p["critic_t"]), s64, a64)[3]) < FWD_TOL
+    (da,) = critic.action_gradients(s, a)
+    assert rel(da, O.critic_action_grads(f64(p["critic"]), s64, a64)) < GRAD_TOL
+    # the last piece (37 rows) equals the same rows in a call of their own
+    assert np.array_equal(mu[2 * B:], actor.predict(s[2 * B:]))
+    assert np.array_equal(q[2 * B:], critic.predict(s[2 * B:], a[2 * B:]))
+    y = np.zeros((B + 1, 1), np.float32)
+    for n in (0, B + 1):
+        with pytest.raises(ValueError, match="outside"):
+            critic.train(s[:n], a[:n], y[:n])
+        with pytest.raises(ValueError, match="outside"):
+            actor.train(s[:n], a[:n])
+    sess.close()
+
+
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_train_methods_parity(dd, O, name):
     """critic.train -> action_gradients -> actor.train, 3 rounds, vs oracle."""
