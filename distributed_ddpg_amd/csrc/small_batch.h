@@ -698,11 +698,16 @@ __global__ __launch_bounds__(SB_NT) void sb_phase3_kernel(SbArgs g) {
 // tanh(elu(elu(s W1 + b1) W2 + b2) W3) is written straight to pinned host
 // memory (no download launch); one workgroup per 4 rows.
 constexpr int SB_PRED_MAX = 256;  // floats of state in the kernel arguments
+constexpr int SB_PRED_BLOCKS = (SB_PRED_MAX + SB_R - 1) / SB_R;  // at most (S >= 1)
 struct SbPredIn {
   float s[SB_PRED_MAX];
 };
+// done (or null): each block, once its actions are visible to the host,
+// stores seq to done[blockIdx.x] (pinned coherent memory) -- the host polls
+// those words instead of waiting for the kernel's completion signal.
 __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const float* base,
-                                                                 SbPredIn in, float* out) {
+                                                                 SbPredIn in, float* out,
+                                                                 unsigned* done, unsigned seq) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * SB_R;
@@ -728,6 +733,11 @@ __global__ __launch_bounds__(SB_NT) void sb_actor_predict_kernel(SbArgs g, const
   for (int idx = tid; idx < 4 * g.A; idx += SB_NT) {
     const int a = idx >> 2, r = idx & 3;
     if (r < valid) out[(size_t)(r0 + r) * g.A + a] = __fmul_rn(o[idx], g.scale);
+  }
+  if (done) {
+    __threadfence_system();  // this thread's actions written back to host memory
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(done + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

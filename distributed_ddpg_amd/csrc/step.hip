@@ -2,6 +2,8 @@
 // forward, critic train, dQ/da, actor train, Adam + soft update, the fused
 // step (gather, hipGraph capture and replay, the small-batch path) and the
 // 1:1 reference methods of networks.py.  DESIGN.md §1, §4, §5.
+#include <atomic>
+#include <chrono>
 #include <functional>
 #include "ctx.h"
 #include "kernels.h"
@@ -1257,6 +1259,8 @@ void sb_setup(ddpg_ctx* c) {
     HIP_TRY(hipFuncSetAttribute((const void*)sb_actor_predict_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     HIP_TRY(hipHostMalloc(&c->h_pred, (size_t)c->Bmax * c->A * sizeof(float)));
+    HIP_TRY(hipHostMalloc(&c->h_pred_done, SB_PRED_BLOCKS * sizeof(unsigned), hipHostMallocCoherent));
+    memset(c->h_pred_done, 0, SB_PRED_BLOCKS * sizeof(unsigned));
     c->sb_ok = true;
   }
 }
@@ -1276,13 +1280,40 @@ int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_
       memcpy(in.s, s, sizeof(float) * B * c->S);
       const SbArgs a = sb_args(c, nullptr, B, 1.f);
       const size_t smem = (SB_RED + 2 * SB_BIAS + 8 * (size_t)a.LX + 8 * (size_t)a.LW) * 4;
+      const int nb = ceil_div(B, SB_R);
+      const bool spin = c->sw.pred_spin && c->h_pred_done;
+      unsigned seq = ++c->pred_seq;
+      if (seq == 0) seq = c->pred_seq = 1;  // 0 is the words' initial value
       {
         ProfScope ps(c, "sb_actor_predict", 0, 0);
-        hipLaunchKernelGGL(sb_actor_predict_kernel, dim3(ceil_div(B, SB_R)), dim3(SB_NT), smem,
-                           c->stream, a, target ? c->target : c->theta, in, c->h_pred);
+        hipLaunchKernelGGL(sb_actor_predict_kernel, dim3(nb), dim3(SB_NT), smem, c->stream, a,
+                           target ? c->target : c->theta, in, c->h_pred,
+                           spin ? c->h_pred_done : nullptr, seq);
         HIP_TRY(hipGetLastError());
       }
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (spin) {
+        // poll the blocks' completion words (the kernel may queue behind an
+        // asynchronous learner step: after 50 ms fall back to the stream wait,
+        // which also surfaces a kernel fault)
+        const volatile unsigned* d = c->h_pred_done;
+        const auto t0 = std::chrono::steady_clock::now();
+        int b = 0;
+        while (b < nb) {
+          if (d[b] == seq) {
+            ++b;
+            continue;
+          }
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            for (; b < nb; ++b)
+              if (d[b] != seq) throw einval("action selection: block %d did not complete", b);
+            break;
+          }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+      } else {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+      }
       memcpy(a_out, c->h_pred, sizeof(float) * B * c->A);
       return;
     }

@@ -90,6 +90,12 @@ class Session:
         self.cfg = cfg
         self.ctx = _lib.ctypes.c_void_p()
         check(lib.ddpg_create(_lib.ctypes.byref(cfg), _lib.ctypes.byref(self.ctx)))
+        # action selection's host staging: ctypes arrays passed as they are
+        # (numpy's .ctypes pointer conversion costs microseconds per call)
+        self._io_in = (_lib.ctypes.c_float * _IO_FLOATS)()
+        self._io_out = (_lib.ctypes.c_float * _IO_FLOATS)()
+        self._io_in_np = np.frombuffer(self._io_in, np.float32)
+        self._io_out_np = np.frombuffer(self._io_out, np.float32)
 
     # --- tf.Session-like
     def run(self, fetches, feed_dict=None):
@@ -184,10 +190,29 @@ class Session:
     def _pieces(self, B):
         return [(i, min(B, i + self.batch_max)) for i in range(0, B, self.batch_max)]
 
+    def _rowwise(self, fn, ins, width):
+        """[B, width] fp32 result of fn(inputs, n, out) over row pieces of at
+        most batch_max rows (one direct call when B fits: action selection
+        pays no extra copy)."""
+        B = ins[0].shape[0]
+        out = np.empty((B, width), np.float32)
+        if 0 < B <= self.batch_max:
+            fn(ins, B, out)
+            return out
+        for i, j in self._pieces(B):
+            op = np.empty((j - i, width), np.float32)
+            fn([np.ascontiguousarray(x[i:j]) for x in ins], j - i, op)
+            out[i:j] = op
+        return out
+
+
+_IO_FLOATS = 4096  # staging floats for small forward calls (Session._io_*)
+
 
 def _transform(scaler, x):
-    x = np.asarray(x, dtype=np.float64)
-    return scaler.transform(x) if scaler is not None else x
+    # without a scaler the rows go straight to the fp32 feed cast, as the
+    # reference's preprocess_input returns them unchanged (networks.py:65-69)
+    return scaler.transform(np.asarray(x, dtype=np.float64)) if scaler is not None else x
 
 
 class ActorNetwork:
@@ -222,12 +247,16 @@ class ActorNetwork:
     def _forward(self, inputs, target):
         ss = self.sess
         s = ss._rows(self.preprocess_input(inputs), self.s_dim, any_batch=True)
-        out = np.empty((s.shape[0], self.a_dim), np.float32)
-        for i, j in ss._pieces(s.shape[0]):
-            sp, op = np.ascontiguousarray(s[i:j]), np.empty((j - i, self.a_dim), np.float32)
-            check(lib.ddpg_actor_forward(ss.ctx, int(target), fptr(sp), j - i, fptr(op)), ss.ctx)
-            out[i:j] = op
-        return out
+        B, S, A = s.shape[0], self.s_dim, self.a_dim
+        if 0 < B <= ss.batch_max and B * max(S, A) <= _IO_FLOATS:
+            # action selection (ddpg.py:68-70): staged through the session's
+            # ctypes arrays
+            ss._io_in_np[:B * S] = s.reshape(-1)
+            check(lib.ddpg_actor_forward(ss.ctx, int(target), ss._io_in, B, ss._io_out), ss.ctx)
+            return ss._io_out_np[:B * A].reshape(B, A).copy()
+        fn = lambda x, n, o: check(lib.ddpg_actor_forward(ss.ctx, int(target), fptr(x[0]), n,
+                                                          fptr(o)), ss.ctx)
+        return ss._rowwise(fn, [s], A)
 
     def predict(self, inputs):
         return self._forward(inputs, False)
@@ -290,16 +319,10 @@ class CriticNetwork:
     def _forward(self, inputs, action, target):
         ss = self.sess
         s = ss._rows(self.preprocess_input(inputs), self.s_dim, any_batch=True)
-        B = s.shape[0]
-        a = f32(action).reshape(B, self.a_dim)
-        q = np.empty((B, 1), np.float32)
-        for i, j in ss._pieces(B):
-            sp, ap = np.ascontiguousarray(s[i:j]), np.ascontiguousarray(a[i:j])
-            qp = np.empty((j - i, 1), np.float32)
-            check(lib.ddpg_critic_forward(ss.ctx, int(target), fptr(sp), fptr(ap), j - i, fptr(qp)),
-                  ss.ctx)
-            q[i:j] = qp
-        return q
+        a = f32(action).reshape(s.shape[0], self.a_dim)
+        fn = lambda x, n, o: check(lib.ddpg_critic_forward(ss.ctx, int(target), fptr(x[0]),
+                                                           fptr(x[1]), n, fptr(o)), ss.ctx)
+        return ss._rowwise(fn, [s, a], 1)
 
     def predict(self, inputs, action):
         return self._forward(inputs, action, False)
@@ -311,15 +334,11 @@ class CriticNetwork:
         """networks.py:189-193: list of one [B, A] array (grad_ys = 1)."""
         ss = self.sess
         s = ss._rows(self.preprocess_input(inputs), self.s_dim, any_batch=True)
-        B = s.shape[0]
-        a = f32(actions).reshape(B, self.a_dim)
-        da = np.empty((B, self.a_dim), np.float32)
-        for i, j in ss._pieces(B):  # grad_ys = 1 per row: rows independent
-            sp, ap = np.ascontiguousarray(s[i:j]), np.ascontiguousarray(a[i:j])
-            dp = np.empty((j - i, self.a_dim), np.float32)
-            check(lib.ddpg_critic_action_grad(ss.ctx, fptr(sp), fptr(ap), j - i, fptr(dp)), ss.ctx)
-            da[i:j] = dp
-        return [da]
+        a = f32(actions).reshape(s.shape[0], self.a_dim)
+        # grad_ys = 1 per row: the rows are independent
+        fn = lambda x, n, o: check(lib.ddpg_critic_action_grad(ss.ctx, fptr(x[0]), fptr(x[1]), n,
+                                                               fptr(o)), ss.ctx)
+        return [ss._rowwise(fn, [s, a], self.a_dim)]
 
     def update_target_network(self):
         check(lib.ddpg_soft_update(self.sess.ctx, _lib.SOFT_CRITIC), self.sess.ctx)

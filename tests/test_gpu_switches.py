@@ -66,7 +66,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
             "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW",
-            "DDPG_FWD_PACK", "DDPG_GATHER16")
+            "DDPG_FWD_PACK", "DDPG_GATHER16", "DDPG_PRED_SPIN")
 
 
 @pytest.fixture(scope="module")
@@ -570,3 +570,33 @@ def test_slots_in_place_ring_reuse_pipelined(dd, O, monkeypatch, name):
     for x, y in zip(got[0], ref[0]):
         for u, v in zip(x, y):
             assert np.array_equal(u, v)
+
+
+@pytest.mark.parametrize("name", ["ip", "odd"])
+def test_pred_spin_bitwise(dd, O, monkeypatch, name):
+    """Action selection (sb_actor_predict) returns once the host sees every
+    block's completion word by default, after hipStreamSynchronize with
+    DDPG_PRED_SPIN=0: the same actions, bit for bit -- also when the call
+    queues behind an asynchronous fused step (the worker's pipelined loop)."""
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    st = np.random.default_rng(4).standard_normal((B, S)).astype(np.float32)
+    outs = []
+    for spin in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_PRED_SPIN", spin)
+        sess, actor, critic = _session(dd, O, name, p)
+        rb = ReplayBuffer(5000, 1234)
+        _fill(rb, S, A, 3000, scale, seed=2)
+        fl = FusedLearner(sess, rb, B)
+        got = [actor.predict(st[:1]), actor.predict(st), actor.predict_target(st[:3])]
+        for _ in range(3):
+            fl.step()  # no stats: nothing waits for it
+            got.append(actor.predict(st[:1]))
+        got.append(actor.predict(st))
+        outs.append(got)
+        sess.close()
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y)
