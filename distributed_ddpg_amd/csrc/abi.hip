@@ -36,6 +36,7 @@ static void ctx_free(ddpg_ctx* c) {
   if (c->h_slots) (void)hipHostFree(c->h_slots);
   if (c->h_pred) (void)hipHostFree(c->h_pred);
   if (c->h_pred_done) (void)hipHostFree(c->h_pred_done);
+  if (c->h_stats_word) (void)hipHostFree(c->h_stats_word);
   for (auto& g : c->gslot) {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (g.h_idx) (void)hipHostFree(g.h_idx);
@@ -174,6 +175,7 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
       c->sw.fwd_pack = !env_is("DDPG_FWD_PACK", "0");
       c->sw.gather16 = !env_is("DDPG_GATHER16", "0");
       c->sw.pred_spin = !env_is("DDPG_PRED_SPIN", "0");
+      c->sw.stats_spin = !env_is("DDPG_STATS_SPIN", "0");
       c->sw.half_twin = !env_is("DDPG_HALF_TWIN", "0");
       c->sw.skinny_nl = !env_is("DDPG_SKINNY_NL", "0");
       c->sw.prof_shapes = env_is("DDPG_PROF_SHAPES", "1");

@@ -260,6 +260,8 @@ struct ddpg_ctx {
   size_t sb_smem = 0;         // dynamic LDS bytes of the phase kernels
   unsigned* h_pred_done = nullptr;  // pinned coherent [SB_PRED_BLOCKS]: per-block completion seq
   unsigned pred_seq = 0;
+  unsigned* h_stats_word = nullptr;  // pinned coherent: [0] completion word, then 2 floats
+  unsigned stats_seq = 0;
   float* h_pred = nullptr;    // pinned [Bmax][A]: action-selection output (written by the GPU)
   int td_nqt = 0;      // fused step: target-critic partials pending in qpart_t for critic_loss
   int sb_xstride = 0;  // XCD packing of the phase kernels: 0 auto (on up to 32 workgroups),
@@ -290,6 +292,7 @@ struct ddpg_ctx {
     bool half_twin = true;   // DDPG_HALF_TWIN=0: bf16 config stores cat2 / dcat state halves in fp32 too
     bool gemm_pack = true;   // DDPG_GEMM_PACK=0: deferred GEMMs launched one by one
     bool fwd_pack = true;    // DDPG_FWD_PACK=0: the step's forward layers in sequence
+    bool stats_spin = true;  // DDPG_STATS_SPIN=0: stats read back by a copy + hipStreamSynchronize
     bool pred_spin = true;   // DDPG_PRED_SPIN=0: action selection waits with hipStreamSynchronize
     bool gather16 = true;    // DDPG_GATHER16=0: the one-row-per-wave gather everywhere
     bool tk_fwd = true;      // DDPG_TK_FWD=0: thin_k's generic epilogue for forward parts too

@@ -764,6 +764,18 @@ DDPG_DEV void advance_powers(float* pw, int mask, float b1, float b2) {
     }
 }
 
+// A synchronous call's stats (q_max, loss) to pinned coherent host memory,
+// then the call's sequence number to its completion word with a system-scope
+// release: the host polls the word instead of a copy plus a stream wait.
+__global__ void stats_out_kernel(const float* __restrict__ st, float* out, unsigned* word,
+                                 unsigned seq) {
+  if (threadIdx.x == 0) {
+    out[0] = st[0];
+    out[1] = st[1];
+    __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void advance_powers_kernel(float* pw, int mask, float b1, float b2) {
   advance_powers(pw, mask, b1, b2);
 }

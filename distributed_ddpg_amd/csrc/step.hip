@@ -1146,6 +1146,53 @@ static void check_b(ddpg_ctx* c, int B) {
   if (B <= 0 || B > c->Bmax) throw einval("batch %d outside [1, %d]", B, c->Bmax);
 }
 
+// Wait until every word w[0 .. n) reads seq (written by a kernel on c->stream
+// after a system-scope release).  The kernel may queue behind asynchronous
+// work: after 50 ms fall back to the stream wait, which also surfaces a fault.
+static void wait_words(ddpg_ctx* c, const volatile unsigned* w, int n, unsigned seq) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int b = 0;
+  while (b < n) {
+    if (w[b] == seq) {
+      ++b;
+      continue;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (; b < n; ++b)
+        if (w[b] != seq) throw einval("completion word %d never written", b);
+      break;
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+}
+
+static unsigned next_seq(unsigned& s) {
+  if (++s == 0) s = 1;  // 0 is the words' initial value
+  return s;
+}
+
+// The stats (q_max, loss) of the work queued so far, synchronously.
+static void read_stats(ddpg_ctx* c, float st[2]) {
+  if (c->sw.stats_spin) {
+    if (!c->h_stats_word) {
+      HIP_TRY(hipHostMalloc(&c->h_stats_word, 4 * sizeof(unsigned), hipHostMallocCoherent));
+      memset(c->h_stats_word, 0, 4 * sizeof(unsigned));
+    }
+    const unsigned seq = next_seq(c->stats_seq);
+    float* out = reinterpret_cast<float*>(c->h_stats_word + 1);
+    hipLaunchKernelGGL(stats_out_kernel, dim3(1), dim3(64), 0, c->stream, c->dstats, out,
+                       c->h_stats_word, seq);
+    HIP_TRY(hipGetLastError());
+    wait_words(c, c->h_stats_word, 1, seq);
+    st[0] = out[0];
+    st[1] = out[1];
+    return;
+  }
+  HIP_TRY(hipMemcpyAsync(st, c->dstats, 2 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+}
+
 // ddpg_create's small-batch part (small_batch.h): whether the dims fit the
 // phase kernels' LDS budget, the saved-tensor layout, the weight-gradient
 // tables and the W^T shadows.  world > 1 never takes the small path.
@@ -1282,8 +1329,7 @@ int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_
       const size_t smem = (SB_RED + 2 * SB_BIAS + 8 * (size_t)a.LX + 8 * (size_t)a.LW) * 4;
       const int nb = ceil_div(B, SB_R);
       const bool spin = c->sw.pred_spin && c->h_pred_done;
-      unsigned seq = ++c->pred_seq;
-      if (seq == 0) seq = c->pred_seq = 1;  // 0 is the words' initial value
+      const unsigned seq = next_seq(c->pred_seq);
       {
         ProfScope ps(c, "sb_actor_predict", 0, 0);
         hipLaunchKernelGGL(sb_actor_predict_kernel, dim3(nb), dim3(SB_NT), smem, c->stream, a,
@@ -1291,29 +1337,10 @@ int ddpg_actor_forward(ddpg_ctx* c, int target, const float* s, int B, float* a_
                            spin ? c->h_pred_done : nullptr, seq);
         HIP_TRY(hipGetLastError());
       }
-      if (spin) {
-        // poll the blocks' completion words (the kernel may queue behind an
-        // asynchronous learner step: after 50 ms fall back to the stream wait,
-        // which also surfaces a kernel fault)
-        const volatile unsigned* d = c->h_pred_done;
-        const auto t0 = std::chrono::steady_clock::now();
-        int b = 0;
-        while (b < nb) {
-          if (d[b] == seq) {
-            ++b;
-            continue;
-          }
-          if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            for (; b < nb; ++b)
-              if (d[b] != seq) throw einval("action selection: block %d did not complete", b);
-            break;
-          }
-        }
-        std::atomic_thread_fence(std::memory_order_acquire);
-      } else {
+      if (spin)  // the blocks' completion words
+        wait_words(c, c->h_pred_done, nb, seq);
+      else
         HIP_TRY(hipStreamSynchronize(c->stream));
-      }
       memcpy(a_out, c->h_pred, sizeof(float) * B * c->A);
       return;
     }
@@ -1352,8 +1379,7 @@ int ddpg_critic_train(ddpg_ctx* c, const float* s, const float* a, const float* 
     if (q_pre) download_rows(c, q_pre, c->q, 1, B, 1);
     if (loss) {
       float st[2];
-      HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      read_stats(c, st);
       *loss = st[1];
     }
   });
@@ -1553,8 +1579,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
     c->sb_shadow_ok = false;
   if (stats) {
     float st[2];
-    HIP_TRY(hipMemcpyAsync(st, c->dstats, sizeof st, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    read_stats(c, st);
     stats->q_max = st[0];
     stats->loss = st[1];
   }

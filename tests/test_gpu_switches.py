@@ -54,7 +54,7 @@ import random
 import numpy as np
 import pytest
 
-from test_gpu_parity import (CONFIGS, GRAD_TOL, FWD_TOL, _fill, _params, _session,
+from test_gpu_parity import (CONFIGS, GRAD_TOL, FWD_TOL, _batch, _fill, _params, _session,
                              _session_dtype, assert_steps_close, f64, rel)
 
 pytestmark = pytest.mark.gpu
@@ -66,7 +66,8 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_GRAPH_COMM", "DDPG_TEST_CS_SPIN", "DDPG_KCOMB_SPLITS", "DDPG_TK_FWD",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
             "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW",
-            "DDPG_FWD_PACK", "DDPG_GATHER16", "DDPG_PRED_SPIN")
+            "DDPG_FWD_PACK", "DDPG_GATHER16", "DDPG_PRED_SPIN",
+            "DDPG_STATS_SPIN")
 
 
 @pytest.fixture(scope="module")
@@ -600,3 +601,36 @@ def test_pred_spin_bitwise(dd, O, monkeypatch, name):
         sess.close()
     for x, y in zip(*outs):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("name", ["ip", "wide"])
+def test_stats_spin_bitwise(dd, O, monkeypatch, name):
+    """Synchronous stats (fused step with stats, critic.train's loss): by
+    default a one-thread kernel writes them to pinned host memory and the host
+    polls its completion word, with DDPG_STATS_SPIN=0 a device-to-host copy
+    and a stream wait -- the same values and states, bit for bit, including
+    stats read right after asynchronous steps."""
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    outs = []
+    for spin in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_STATS_SPIN", spin)
+        r = _run(dd, O, name, p, 3)
+        from distributed_ddpg_amd.learner import FusedLearner
+        from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+        sess, actor, critic = _session(dd, O, name, p)
+        rb = ReplayBuffer(5000, 1234)
+        _fill(rb, S, A, 3000, scale, seed=2)
+        fl = FusedLearner(sess, rb, B)
+        fl.step()
+        fl.step()  # asynchronous, then a synchronous read behind them
+        st = fl.step(stats=True)
+        s_, a_, _r = _batch(name, seed=6)
+        y = np.random.default_rng(6).standard_normal((B, 1)).astype(np.float32)
+        q, _, loss = critic.train(s_, a_, y)
+        sess.close()
+        outs.append((r, st, q, loss))
+    (r0, st0, q0, l0), (r1, st1, q1, l1) = outs
+    _bitwise(r0, r1)
+    assert st0 == st1 and np.array_equal(q0, q1) and l0 == l1
