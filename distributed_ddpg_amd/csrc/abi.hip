@@ -37,6 +37,7 @@ static void ctx_free(ddpg_ctx* c) {
   if (c->h_pred) (void)hipHostFree(c->h_pred);
   if (c->h_pred_done) (void)hipHostFree(c->h_pred_done);
   if (c->h_stats_word) (void)hipHostFree(c->h_stats_word);
+  if (c->h_rows_word) (void)hipHostFree(c->h_rows_word);
   for (auto& g : c->gslot) {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (g.h_idx) (void)hipHostFree(g.h_idx);

@@ -262,6 +262,8 @@ struct ddpg_ctx {
   unsigned pred_seq = 0;
   unsigned* h_stats_word = nullptr;  // pinned coherent: [0] completion word, then 2 floats
   unsigned stats_seq = 0;
+  unsigned* h_rows_word = nullptr;  // pinned coherent: [0] completion word, floats from [16]
+  unsigned rows_seq = 0;
   float* h_pred = nullptr;    // pinned [Bmax][A]: action-selection output (written by the GPU)
   int td_nqt = 0;      // fused step: target-critic partials pending in qpart_t for critic_loss
   int sb_xstride = 0;  // XCD packing of the phase kernels: 0 auto (on up to 32 workgroups),

@@ -776,6 +776,21 @@ __global__ void stats_out_kernel(const float* __restrict__ st, float* out, unsig
   }
 }
 
+// A small row block [B][cols] (leading dimension ld) to pinned coherent host
+// memory, then the call's completion word (system-scope release): the 1:1
+// methods' small results without a staged copy into pageable memory.
+__global__ __launch_bounds__(256) void rows_out_kernel(const float* __restrict__ src, int ld,
+                                                       int B, int cols, float* out,
+                                                       unsigned* word, unsigned seq) {
+  for (int i = threadIdx.x; i < B * cols; i += 256) {
+    const int r = i / cols;
+    out[i] = src[(size_t)r * ld + (i - r * cols)];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void advance_powers_kernel(float* pw, int mask, float b1, float b2) {
   advance_powers(pw, mask, b1, b2);
 }

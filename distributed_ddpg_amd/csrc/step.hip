@@ -1135,8 +1135,26 @@ static void upload_rows(ddpg_ctx* c, float* dst, int ld, const float* src, int B
     HIP_TRY(hipGetLastError());
   }
 }
+static void wait_words(ddpg_ctx* c, const volatile unsigned* w, int n, unsigned seq);
+static unsigned next_seq(unsigned& s);
+constexpr int kRowsOutMax = 4096;  // floats: small results through pinned memory
 static void download_rows(ddpg_ctx* c, float* dst, const float* src, int ld, int B, int cols) {
   if (B <= 0 || cols <= 0) return;
+  if (c->sw.stats_spin && (size_t)B * cols <= kRowsOutMax) {
+    if (!c->h_rows_word) {
+      HIP_TRY(hipHostMalloc(&c->h_rows_word, (16 + kRowsOutMax) * sizeof(unsigned),
+                            hipHostMallocCoherent));
+      memset(c->h_rows_word, 0, 16 * sizeof(unsigned));
+    }
+    const unsigned seq = next_seq(c->rows_seq);
+    float* out = reinterpret_cast<float*>(c->h_rows_word + 16);
+    hipLaunchKernelGGL(rows_out_kernel, dim3(1), dim3(256), 0, c->stream, src, ld, B, cols, out,
+                       c->h_rows_word, seq);
+    HIP_TRY(hipGetLastError());
+    wait_words(c, c->h_rows_word, 1, seq);
+    memcpy(dst, out, sizeof(float) * B * cols);
+    return;
+  }
   HIP_TRY(hipMemcpy2DAsync(dst, (size_t)cols * 4, src, (size_t)ld * 4, (size_t)cols * 4, B,
                            hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
