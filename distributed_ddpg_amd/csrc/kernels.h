@@ -791,6 +791,20 @@ __global__ __launch_bounds__(256) void rows_out_kernel(const float* __restrict__
   if (threadIdx.x == 0) __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A small row block [B][cols] uploaded in the kernel arguments (no staged
+// copy from pageable memory): dst rows (leading dimension ld) get the values.
+constexpr int kRowsInMax = 256;  // floats
+struct RowsIn {
+  float v[kRowsInMax];
+};
+__global__ __launch_bounds__(256) void rows_in_kernel(RowsIn in, float* __restrict__ dst, int ld,
+                                                      int B, int cols) {
+  for (int i = threadIdx.x; i < B * cols; i += 256) {
+    const int r = i / cols;
+    dst[(size_t)r * ld + (i - r * cols)] = in.v[i];
+  }
+}
+
 __global__ void advance_powers_kernel(float* pw, int mask, float b1, float b2) {
   advance_powers(pw, mask, b1, b2);
 }

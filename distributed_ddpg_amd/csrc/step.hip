@@ -1126,8 +1126,16 @@ static void learner_step_any(ddpg_ctx* c, ddpg_replay* rb, int B, float inv_b) {
 // ====================================================================== helpers
 static void upload_rows(ddpg_ctx* c, float* dst, int ld, const float* src, int B, int cols) {
   if (B <= 0 || cols <= 0) return;
-  HIP_TRY(hipMemcpy2DAsync(dst, (size_t)ld * 4, src, (size_t)cols * 4, (size_t)cols * 4, B,
-                           hipMemcpyHostToDevice, c->stream));
+  if (c->sw.stats_spin && (size_t)B * cols <= kRowsInMax) {
+    // small rows (the 1:1 methods at small batch) in the kernel arguments
+    RowsIn in;
+    memcpy(in.v, src, sizeof(float) * B * cols);
+    hipLaunchKernelGGL(rows_in_kernel, dim3(1), dim3(256), 0, c->stream, in, dst, ld, B, cols);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemcpy2DAsync(dst, (size_t)ld * 4, src, (size_t)cols * 4, (size_t)cols * 4, B,
+                             hipMemcpyHostToDevice, c->stream));
+  }
   const Twin t = act_twin(c, dst);
   if (t.p) {  // the twin covers the padded rows (pads are zero in both)
     hipLaunchKernelGGL(twin_kernel, dim3(std::min(ceil_div(B * ld, 256), 2048)), dim3(256), 0,
