@@ -137,6 +137,12 @@ struct ddpg_replay {
   // recorded by learner contexts after their gather; ring writes wait on it so
   // a queued gather never reads rows that a later add overwrote
   hipEvent_t last_read = nullptr;
+  // small flushes (a worker's few rows per step) travel in a kernel's
+  // arguments, asynchronously; learner steps wait on `written` before their
+  // gather.  DDPG_RING_ARGS=0: copies from the host staging plus a stream wait.
+  hipEvent_t written = nullptr;
+  hipStream_t written_on = nullptr;  // stream `written` was last recorded on
+  bool args_flush = true;
   explicit ddpg_replay(int64_t seed) : sampler(seed) {}
   size_t es() const { return f64 ? 8 : 4; }  // bytes per s / s2 / r element
   unsigned char* ps() const { return f64 ? (unsigned char*)rsd : (unsigned char*)rs; }
@@ -144,7 +150,9 @@ struct ddpg_replay {
   unsigned char* pr() const { return f64 ? (unsigned char*)rrd : (unsigned char*)rr; }
 };
 
-void replay_flush(ddpg_replay* rb);
+// on: the stream of the learner step about to read the ring (the small,
+// kernel-argument form then runs in that stream's order), or null
+void replay_flush(ddpg_replay* rb, hipStream_t on = nullptr);
 
 // ====================================================================== context
 // a GEMM queued under gemm_defer (gemm_flush)

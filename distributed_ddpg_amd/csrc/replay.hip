@@ -65,6 +65,9 @@ static int replay_create_impl(int device, int S, int A, int64_t cap, int64_t see
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&rb->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&rb->last_read, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&rb->written, hipEventDisableTiming));
+    const char* ra_env = getenv("DDPG_RING_ARGS");
+    rb->args_flush = !(ra_env && strcmp(ra_env, "0") == 0);
     const size_t c = (size_t)cap, es = rb->es();
     void *ps, *ps2, *pr;
     HIP_TRY(hipMalloc(&ps, c * S * es));
@@ -111,12 +114,14 @@ void ddpg_replay_destroy(ddpg_replay* rb) {
   if (!rb) return;
   (void)hipSetDevice(rb->device);
   if (rb->stream) (void)hipStreamSynchronize(rb->stream);
+  if (rb->written_on) (void)hipEventSynchronize(rb->written);
   for (void* p : {(void*)rb->rs, (void*)rb->rs2, (void*)rb->rr, (void*)rb->rsd, (void*)rb->rs2d,
                   (void*)rb->rrd, (void*)rb->ra, (void*)rb->rt, (void*)rb->d_slots,
                   (void*)rb->d_tmp})
     if (p) (void)hipFree(p);
   if (rb->stream) (void)hipStreamDestroy(rb->stream);
   if (rb->last_read) (void)hipEventDestroy(rb->last_read);
+  if (rb->written) (void)hipEventDestroy(rb->written);
   delete rb;
 }
 
@@ -147,10 +152,77 @@ static void ring_write(ddpg_replay* rb, int64_t first, int n, const void* s, con
   }
 }
 
+// A few staged rows written into the ring by one block, the rows in the
+// kernel arguments ([s rows][s2 rows][r][a][t] as 32-bit words, s / s2 / r in
+// the ring's precision): the host staging is free again when the launch call
+// returns, so the flush needs no host wait.
+constexpr int kRingArgWords = 512;
+struct RingRowsIn {
+  unsigned w[kRingArgWords];
+};
+__global__ __launch_bounds__(256) void ring_rows_kernel(RingRowsIn in, int n, long long first,
+                                                        long long cap, int sw, int rw, int A,
+                                                        unsigned* __restrict__ ps,
+                                                        unsigned* __restrict__ ps2,
+                                                        unsigned* __restrict__ pr,
+                                                        unsigned* __restrict__ pa,
+                                                        unsigned* __restrict__ pt) {
+  // sw / rw: words per s row / per r value; A words per a row; 1 per t
+  const int seg[5] = {sw, sw, rw, A, 1};
+  unsigned* dst[5] = {ps, ps2, pr, pa, pt};
+  int off = 0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int per = seg[q];
+    for (int i = threadIdx.x; i < n * per; i += 256) {
+      const int row = i / per;
+      const long long slot = (first + row) % cap;
+      dst[q][slot * per + (i - row * per)] = in.w[off + i];
+    }
+    off += n * per;
+  }
+}
+
+// rb->stream's next ring access after the last kernel-argument flush, which
+// may have run on a learner's stream
+static void ring_join(ddpg_replay* rb) {
+  if (rb->written_on && rb->written_on != rb->stream)
+    HIP_TRY(hipStreamWaitEvent(rb->stream, rb->written, 0));
+}
+
 extern "C++" {  // declared in ctx.h (C++ linkage)
-void replay_flush(ddpg_replay* rb) {
+void replay_flush(ddpg_replay* rb, hipStream_t on) {
   if (rb->st_n == 0) return;
+  const size_t es = rb->es(), S = rb->S, A = rb->A, n = (size_t)rb->st_n;
+  const size_t sw = S * es / 4, rw = es / 4;
+  if (rb->args_flush && n * (2 * sw + rw + A + 1) <= (size_t)kRingArgWords) {
+    // the reading learner's own stream when known: its previous gather is
+    // then ordered before these writes, and its next one after them
+    const hipStream_t st = on ? on : rb->stream;
+    if (rb->last_read) HIP_TRY(hipStreamWaitEvent(st, rb->last_read, 0));
+    RingRowsIn in;
+    unsigned char* b = reinterpret_cast<unsigned char*>(in.w);
+    memcpy(b, rb->st_s.data(), n * S * es);
+    b += n * S * es;
+    memcpy(b, rb->st_s2.data(), n * S * es);
+    b += n * S * es;
+    memcpy(b, rb->st_r.data(), n * es);
+    b += n * es;
+    memcpy(b, rb->st_a.data(), n * A * 4);
+    b += n * A * 4;
+    memcpy(b, rb->st_t.data(), n * 4);
+    hipLaunchKernelGGL(ring_rows_kernel, dim3(1), dim3(256), 0, st, in, (int)n,
+                       (long long)rb->st_first, (long long)rb->cap, (int)sw, (int)rw, (int)A,
+                       (unsigned*)rb->ps(), (unsigned*)rb->ps2(), (unsigned*)rb->pr(), (unsigned*)rb->ra,
+                       (unsigned*)rb->rt);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(rb->written, st));
+    rb->written_on = st;
+    rb->st_n = 0;
+    return;
+  }
   if (rb->last_read) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->last_read, 0));
+  ring_join(rb);
   ring_write(rb, rb->st_first, rb->st_n, rb->st_s.data(), rb->st_a.data(), rb->st_r.data(),
              rb->st_t.data(), rb->st_s2.data());
   HIP_TRY(hipStreamSynchronize(rb->stream));  // staging is reused after this
@@ -183,6 +255,7 @@ static void replay_add_impl(ddpg_replay* rb, const T* s, const float* a, const T
   if (n >= kStageRows) {  // bulk insert
     replay_flush(rb);
     if (rb->last_read) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->last_read, 0));
+    ring_join(rb);
     // only the last `cap` rows can survive; skip the ones that would be overwritten
     const int64_t skip = n > rb->cap ? n - rb->cap : 0;
     const size_t m = (size_t)(n - skip);
@@ -242,6 +315,7 @@ int64_t ddpg_replay_total_added(ddpg_replay* rb) { return rb ? rb->total : 0; }
 int ddpg_replay_clear(ddpg_replay* rb) {
   return rguard(rb, [&] {
     HIP_TRY(hipStreamSynchronize(rb->stream));
+    if (rb->written_on) HIP_TRY(hipEventSynchronize(rb->written));
     rb->count = rb->total = 0;
     rb->st_n = 0;
   });
@@ -259,6 +333,7 @@ static int sample_impl(ddpg_replay* rb, int B, T* s, float* a, T* r, uint8_t* t,
     if (B < 0) throw einval("negative batch");
     HIP_TRY(hipSetDevice(rb->device));
     replay_flush(rb);
+    ring_join(rb);
     const int k = (int)std::min<int64_t>(B, rb->count);  // replay_buffer.py:36-39
     rb->tmp_idx.resize(std::max(1, k));
     if (rb->sampler.sample(rb->count, k, rb->tmp_idx.data()) != 0) throw einval("sample failed");

@@ -32,6 +32,7 @@ class ReplayBuffer:
         self.device = int(device)
         self.count = 0
         self._rb = None  # created on first add, when the row dims and precision are known
+        self._one = None  # single-row staging (set up after the first add)
         self.s_dim = self.a_dim = None
         self.f64 = False
 
@@ -61,12 +62,37 @@ class ReplayBuffer:
     # -- reference interface
     def add(self, s, a, r, t, s2):
         """replay_buffer.py:21-28 (one transition)."""
-        s = np.asarray(s)
-        f64 = s.dtype == np.float64 if self._rb is None else self.f64
-        dt = np.float64 if f64 else np.float32
-        self.add_batch(np.asarray(s, dt).reshape(1, -1), np.asarray(a, np.float32).reshape(1, -1),
-                       np.array([r], dt), np.array([bool(t)]),
-                       np.asarray(s2, dt).reshape(1, -1))
+        w = self._one
+        if w is None:
+            s = np.asarray(s)
+            f64 = s.dtype == np.float64 if self._rb is None else self.f64
+            dt = np.float64 if f64 else np.float32
+            self.add_batch(np.asarray(s, dt).reshape(1, -1),
+                           np.asarray(a, np.float32).reshape(1, -1), np.array([r], dt),
+                           np.array([bool(t)]), np.asarray(s2, dt).reshape(1, -1))
+            self._one_setup()
+            return
+        # a worker's per-env-step add: through persistent ctypes arrays
+        # (numpy's .ctypes pointer conversion costs microseconds per array)
+        if np.size(s) != self.s_dim or np.size(s2) != self.s_dim or np.size(a) != self.a_dim:
+            raise ValueError("row dims changed: expected s/s2 of %d and a of %d values" % (
+                self.s_dim, self.a_dim))
+        w["s_np"][:] = np.ravel(s)
+        w["s2_np"][:] = np.ravel(s2)
+        w["a_np"][:] = np.ravel(a)
+        w["r_np"][0] = r
+        w["t"][0] = 1 if t else 0
+        self._err(w["fn"](self._rb, w["s"], w["a"], w["r"], w["t"], w["s2"], 1))
+        self.count = min(self.count + 1, self.buffer_size)
+
+    def _one_setup(self):
+        ct = ctypes.c_double if self.f64 else ctypes.c_float
+        w = {"s": (ct * self.s_dim)(), "s2": (ct * self.s_dim)(), "r": (ct * 1)(),
+             "a": (ctypes.c_float * self.a_dim)(), "t": (ctypes.c_uint8 * 1)(),
+             "fn": lib.ddpg_replay_add_f64 if self.f64 else lib.ddpg_replay_add}
+        for k in ("s", "s2", "r", "a"):
+            w[k + "_np"] = np.ctypeslib.as_array(w[k])
+        self._one = w
 
     def add_batch(self, s, a, r, t, s2):
         """n transitions at once (rows of s, a, r, t, s2)."""

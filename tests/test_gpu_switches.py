@@ -67,7 +67,7 @@ SWITCHES = ("DDPG_XCD", "DDPG_XCD_RECT", "DDPG_PAR", "DDPG_SB_XCD", "DDPG_GEMM",
             "DDPG_PROF_SHAPES", "DDPG_GEMM_PACK", "DDPG_HALF_TWIN", "DDPG_SKINNY_NL",
             "DDPG_GEMM_M16", "DDPG_NW_FUSE", "DDPG_KCOMB_WGRAD", "DDPG_GEMM_HW",
             "DDPG_FWD_PACK", "DDPG_GATHER16", "DDPG_PRED_SPIN",
-            "DDPG_STATS_SPIN")
+            "DDPG_STATS_SPIN", "DDPG_RING_ARGS")
 
 
 @pytest.fixture(scope="module")
@@ -634,3 +634,47 @@ def test_stats_spin_bitwise(dd, O, monkeypatch, name):
     (r0, st0, q0, l0), (r1, st1, q1, l1) = outs
     _bitwise(r0, r1)
     assert st0 == st1 and np.array_equal(q0, q1) and l0 == l1
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_ring_args_bitwise(dd, O, monkeypatch, f64):
+    """A worker's single-row adds (ddpg.py:79-84) interleaved with fused steps,
+    the ring wrapping: by default each flush is one kernel whose arguments
+    carry the rows (no host wait), with DDPG_RING_ARGS=0 copies from the
+    staging plus a stream wait -- the same ring, the same steps, bit for bit;
+    and sample_batch returns exactly the rows added (fp32 and float64 rings)."""
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    name = "ip"
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    rng = np.random.default_rng(9)
+    n = 700
+    dt = np.float64 if f64 else np.float32
+    rows = (rng.standard_normal((n, S)).astype(dt), rng.uniform(-3, 3, (n, A)).astype(np.float32),
+            rng.standard_normal(n).astype(dt), rng.random(n) < 0.05,
+            rng.standard_normal((n, S)).astype(dt))
+    outs = []
+    for v in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_RING_ARGS", v)
+        sess, actor, critic = _session(dd, O, name, p)
+        rb = ReplayBuffer(500, 1234)  # 700 adds: the ring wraps
+        fl = FusedLearner(sess, rb, B)
+        st = []
+        for i in range(n):
+            rb.add(rows[0][i], rows[1][i], rows[2][i], rows[3][i], rows[4][i])
+            if i >= B and i % 3 == 0:
+                st.append(fl.step(stats=i % 2 == 0))
+        s_b, a_b, r_b, t_b, s2_b, pos = rb.sample_batch(64, return_indices=True)
+        ins = (n - rb.size()) + np.asarray(pos)  # insertion index of each sampled row
+        assert np.array_equal(s_b, rows[0][ins]) and np.array_equal(s2_b, rows[4][ins])
+        assert np.array_equal(a_b, rows[1][ins]) and np.array_equal(t_b, rows[3][ins])
+        assert np.array_equal(r_b, rows[2][ins])
+        state = [sess.get_params(w) for w in (0, 1, 2, 3)]
+        sess.close()
+        outs.append((st, state))
+    assert outs[0][0] == outs[1][0]
+    for x, y in zip(outs[0][1], outs[1][1]):
+        for u, w in zip(x, y):
+            assert np.array_equal(u, w)
