@@ -23,7 +23,9 @@ Rank 0 prints ONE JSON line with the contract fields plus
                 sess.run calls per step (oracle/torch_cpu.py) on the host cores: 16
                 threads and 1 thread; + C2 and C1 (B=64), C2 also at os.cpu_count()
   step_latency  p10 / median / p90 of per-step wall time (host sync after each step)
-  small_batch   the InvertedPendulum B=64 latency-bound configuration (N=1 only)
+  small_batch   the InvertedPendulum B=64 latency-bound configuration (N=1 only), with
+                action selection (predict on one state) and the worker's per-env-step
+                device work (predict + one replay add + a step with stats) in us
   c5_bf16       BASELINE configs[4] (S=376, A=17, 2048-wide, B=4096, bf16) (c3 only; every N)
 """
 import argparse
@@ -383,6 +385,23 @@ def action_selection_latency(actor, S, calls=2000):
     return {"batch": 1, "us_per_call": round(1e6 * el / calls, 2), "calls": calls}
 
 
+def worker_env_step_latency(fl, rb, actor, S, n=1000):
+    """The reference worker's device work per env step (ddpg.py:68-113 with
+    the fused learner): actor.predict on one state, ReplayBuffer.add of one
+    transition, learner.step with stats -- host wall time per env step."""
+    st = np.random.default_rng(1).standard_normal((n + 101, S)).astype(np.float32)
+    ts = []
+    for i in range(n + 100):
+        t0 = time.perf_counter()
+        a = actor.predict(st[i:i + 1])
+        rb.add(st[i], a[0], 0.5, False, st[i + 1])
+        fl.step(stats=True)
+        ts.append(1e6 * (time.perf_counter() - t0))
+    p10, p50, p90 = np.percentile(ts[100:], [10, 50, 90])
+    return {"n": n, "p10_us": round(float(p10), 1), "median_us": round(float(p50), 1),
+            "p90_us": round(float(p90), 1)}
+
+
 def pmc_traffic(cfg_name, kernel, launches_per_step):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/*_pmc_<config>.json, written by profiles/pmc_traffic.py from a
@@ -641,7 +660,8 @@ def compact_line(full, limit=CONTRACT_LINE_MAX):
         out["small_batch"] = {k: sb[k] for k in ("value", "ms_per_step", "step_latency",
                                                  "kernels_per_step", "gpu_busy_ms_per_step",
                                                  "launch_overhead_us_per_step",
-                                                 "action_selection") if k in sb}
+                                                 "action_selection", "worker_env_step")
+                             if k in sb}
         b2 = sb.get("b256")
         if b2:
             dp = b2.get("dp_rank0_of_8_weak") or {}
@@ -849,7 +869,8 @@ def main():
             "step_latency": lat2,
             "kernels_per_step": nk2, "gpu_busy_ms_per_step": round(busy2, 4),
             "launch_overhead_us_per_step": round(1000 * (1000 * el2 / 500 - busy2), 1),
-            "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0])}
+            "action_selection": action_selection_latency(actor2, CONFIGS["c2"][0]),
+            "worker_env_step": worker_env_step_latency(fl2, rb2, actor2, CONFIGS["c2"][0])}
         s2.close()
         # the reference's default batch (B = 256): one GPU, and rank 0 of an
         # 8-rank data-parallel run at that per-rank batch (weak: the
