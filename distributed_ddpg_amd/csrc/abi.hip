@@ -1,5 +1,6 @@
 // C-ABI lifecycle (ddpg_create / destroy / sync), parameter I/O, stats
 // readback, profiling and error reporting.  include/ddpg_hip.h.
+#include <atomic>
 #include "ctx.h"
 
 thread_local std::string g_err;
@@ -76,6 +77,8 @@ int ddpg_create(const ddpg_cfg* cfg, ddpg_ctx** out) {
     return DDPG_EINVAL;
   }
   ddpg_ctx* c = new ddpg_ctx();
+  static std::atomic<uint64_t> next_uid{1};
+  c->uid = next_uid++;
   memset(c->slot_ev, 0, sizeof c->slot_ev);
   int rc = guard(c, [&] {
     const ddpg_cfg& k = *cfg;

@@ -141,7 +141,8 @@ struct ddpg_replay {
   // arguments, asynchronously; learner steps wait on `written` before their
   // gather.  DDPG_RING_ARGS=0: copies from the host staging plus a stream wait.
   hipEvent_t written = nullptr;
-  hipStream_t written_on = nullptr;  // stream `written` was last recorded on
+  bool written_rec = false;  // `written` recorded at least once
+  uint64_t written_by = 0;  // ddpg_ctx::uid whose stream `written` was last recorded on
   bool args_flush = true;
   explicit ddpg_replay(int64_t seed) : sampler(seed) {}
   size_t es() const { return f64 ? 8 : 4; }  // bytes per s / s2 / r element
@@ -150,9 +151,10 @@ struct ddpg_replay {
   unsigned char* pr() const { return f64 ? (unsigned char*)rrd : (unsigned char*)rr; }
 };
 
-// on: the stream of the learner step about to read the ring (the small,
-// kernel-argument form then runs in that stream's order), or null
-void replay_flush(ddpg_replay* rb, hipStream_t on = nullptr);
+// on / by: the stream and context uid of the learner step about to read the
+// ring (the small, kernel-argument form then runs in that stream's order), or
+// null / 0
+void replay_flush(ddpg_replay* rb, hipStream_t on = nullptr, uint64_t by = 0);
 
 // ====================================================================== context
 // a GEMM queued under gemm_defer (gemm_flush)
@@ -165,6 +167,7 @@ struct DeferredGemm {
 
 struct ddpg_ctx {
   ddpg_cfg cfg{};
+  uint64_t uid = 0;  // unique per context for the process lifetime (never reused)
   Layout L;
   int S, A, AH1, AH2, CH1, CH2, Bmax;
   int ldS, ldA, ldAH1, ldAH2, ldCH2, ldC;

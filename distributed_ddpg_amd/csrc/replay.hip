@@ -114,7 +114,7 @@ void ddpg_replay_destroy(ddpg_replay* rb) {
   if (!rb) return;
   (void)hipSetDevice(rb->device);
   if (rb->stream) (void)hipStreamSynchronize(rb->stream);
-  if (rb->written_on) (void)hipEventSynchronize(rb->written);
+  if (rb->written) (void)hipEventSynchronize(rb->written);
   for (void* p : {(void*)rb->rs, (void*)rb->rs2, (void*)rb->rr, (void*)rb->rsd, (void*)rb->rs2d,
                   (void*)rb->rrd, (void*)rb->ra, (void*)rb->rt, (void*)rb->d_slots,
                   (void*)rb->d_tmp})
@@ -186,12 +186,11 @@ __global__ __launch_bounds__(256) void ring_rows_kernel(RingRowsIn in, int n, lo
 // rb->stream's next ring access after the last kernel-argument flush, which
 // may have run on a learner's stream
 static void ring_join(ddpg_replay* rb) {
-  if (rb->written_on && rb->written_on != rb->stream)
-    HIP_TRY(hipStreamWaitEvent(rb->stream, rb->written, 0));
+  if (rb->written_rec && rb->written_by) HIP_TRY(hipStreamWaitEvent(rb->stream, rb->written, 0));
 }
 
 extern "C++" {  // declared in ctx.h (C++ linkage)
-void replay_flush(ddpg_replay* rb, hipStream_t on) {
+void replay_flush(ddpg_replay* rb, hipStream_t on, uint64_t by) {
   if (rb->st_n == 0) return;
   const size_t es = rb->es(), S = rb->S, A = rb->A, n = (size_t)rb->st_n;
   const size_t sw = S * es / 4, rw = es / 4;
@@ -217,7 +216,8 @@ void replay_flush(ddpg_replay* rb, hipStream_t on) {
                        (unsigned*)rb->rt);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(rb->written, st));
-    rb->written_on = st;
+    rb->written_by = on ? by : 0;
+    rb->written_rec = true;
     rb->st_n = 0;
     return;
   }
@@ -315,7 +315,7 @@ int64_t ddpg_replay_total_added(ddpg_replay* rb) { return rb ? rb->total : 0; }
 int ddpg_replay_clear(ddpg_replay* rb) {
   return rguard(rb, [&] {
     HIP_TRY(hipStreamSynchronize(rb->stream));
-    if (rb->written_on) HIP_TRY(hipEventSynchronize(rb->written));
+    HIP_TRY(hipEventSynchronize(rb->written));
     rb->count = rb->total = 0;
     rb->st_n = 0;
   });

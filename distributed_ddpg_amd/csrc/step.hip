@@ -1490,7 +1490,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
                         ddpg_stats* stats) {
   // rows flushed asynchronously (replay_flush's kernel-argument form) land
   // before this step's gather
-  if (rb->written_on && rb->written_on != c->stream)
+  if (rb->written_rec && rb->written_by != c->uid)
     HIP_TRY(hipStreamWaitEvent(c->stream, rb->written, 0));
   const int B = Bg / c->world;
   const int64_t* mine = idx + (size_t)c->rank * B;  // this rank's slice of the global draw
@@ -1618,7 +1618,7 @@ static void step_common(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, int Bg
 int ddpg_learner_step(ddpg_ctx* c, ddpg_replay* rb, int Bg, ddpg_stats* stats) {
   return guard(c, [&] {
     if (!rb) throw einval("null replay");
-    replay_flush(rb, c->stream);
+    replay_flush(rb, rb->device == c->cfg.device ? c->stream : nullptr, c->uid);
     check_step(c, rb, Bg, true);
     c->idx_tmp.resize(Bg);
     if (rb->sampler.sample(rb->count, Bg, c->idx_tmp.data()) != 0) throw einval("sample failed");
@@ -1630,7 +1630,7 @@ int ddpg_learner_step_indices(ddpg_ctx* c, ddpg_replay* rb, const int64_t* idx, 
                               ddpg_stats* stats) {
   return guard(c, [&] {
     if (!rb || !idx) throw einval("null argument");
-    replay_flush(rb, c->stream);
+    replay_flush(rb, rb->device == c->cfg.device ? c->stream : nullptr, c->uid);
     check_step(c, rb, Bg, false);
     for (int i = 0; i < Bg; ++i)
       if (idx[i] < 0 || idx[i] >= rb->count) throw einval("index %lld out of range", (long long)idx[i]);

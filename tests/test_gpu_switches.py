@@ -678,3 +678,46 @@ def test_ring_args_bitwise(dd, O, monkeypatch, f64):
     for x, y in zip(outs[0][1], outs[1][1]):
         for u, w in zip(x, y):
             assert np.array_equal(u, w)
+
+
+def test_ring_args_two_learners(dd, O, monkeypatch):
+    """One replay ring read by two learner contexts (two streams) while a
+    worker adds single rows: a flush issued on one learner's stream is joined
+    by the other learner's gather and by sample_batch on the ring's own
+    stream -- the same results as the copy form (DDPG_RING_ARGS=0), bit for
+    bit."""
+    from distributed_ddpg_amd.learner import FusedLearner
+    from distributed_ddpg_amd.replay_buffer import ReplayBuffer
+    name = "ip"
+    S, A, H1, H2, scale, B, _ = CONFIGS[name]
+    p, _ = _params(O, name)
+    rng = np.random.default_rng(12)
+    n = 400
+    rows = (rng.standard_normal((n, S)).astype(np.float32),
+            rng.uniform(-3, 3, (n, A)).astype(np.float32),
+            rng.standard_normal(n).astype(np.float32), rng.random(n) < 0.05,
+            rng.standard_normal((n, S)).astype(np.float32))
+    outs = []
+    for v in ("1", "0"):
+        _clear(monkeypatch)
+        monkeypatch.setenv("DDPG_RING_ARGS", v)
+        s1, _, _ = _session(dd, O, name, p)
+        s2, _, _ = _session(dd, O, name, p)
+        rb = ReplayBuffer(300, 77)
+        f1, f2 = FusedLearner(s1, rb, B), FusedLearner(s2, rb, B)
+        st = []
+        for i in range(n):
+            rb.add(rows[0][i], rows[1][i], rows[2][i], rows[3][i], rows[4][i])
+            if i >= B and i % 2 == 0:
+                st.append((f1 if i % 4 == 0 else f2).step(stats=True))
+        sb = rb.sample_batch(32, return_indices=True)
+        state = [x.get_params(w) for x in (s1, s2) for w in (0, 1)]
+        s1.close()
+        s2.close()
+        outs.append((st, sb, state))
+    assert outs[0][0] == outs[1][0]
+    for x, y in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(x, y)
+    for x, y in zip(outs[0][2], outs[1][2]):
+        for u, w in zip(x, y):
+            assert np.array_equal(u, w)
