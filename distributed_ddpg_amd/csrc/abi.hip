@@ -303,9 +303,7 @@ void ddpg_destroy(ddpg_ctx* c) {
 }
 
 int ddpg_sync(ddpg_ctx* c) {
-  return guard(c, [&] {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-  });
+  return guard(c, [&] { sync_stream(c); });
 }
 
 int ddpg_set_stream(ddpg_ctx* c, void* s) {

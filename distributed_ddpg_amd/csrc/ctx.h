@@ -154,6 +154,9 @@ struct ddpg_replay {
 // on / by: the stream and context uid of the learner step about to read the
 // ring (the small, kernel-argument form then runs in that stream's order), or
 // null / 0
+// ddpg_sync (step.hip): everything queued on c->stream has finished
+struct ddpg_ctx;
+void sync_stream(ddpg_ctx* c);
 void replay_flush(ddpg_replay* rb, hipStream_t on = nullptr, uint64_t by = 0);
 
 // ====================================================================== context

@@ -805,6 +805,11 @@ __global__ __launch_bounds__(256) void rows_in_kernel(RowsIn in, float* __restri
   }
 }
 
+// ddpg_sync's completion word: everything queued before it has finished
+__global__ void word_kernel(unsigned* word, unsigned seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void advance_powers_kernel(float* pw, int mask, float b1, float b2) {
   advance_powers(pw, mask, b1, b2);
 }

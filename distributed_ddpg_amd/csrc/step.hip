@@ -1198,13 +1198,31 @@ static unsigned next_seq(unsigned& s) {
   return s;
 }
 
+static void stats_words_alloc(ddpg_ctx* c) {
+  if (!c->h_stats_word) {
+    HIP_TRY(hipHostMalloc(&c->h_stats_word, 4 * sizeof(unsigned), hipHostMallocCoherent));
+    memset(c->h_stats_word, 0, 4 * sizeof(unsigned));
+  }
+}
+
+// ddpg_sync: a completion word after the queued work, polled (the stream
+// wait with DDPG_STATS_SPIN=0)
+void sync_stream(ddpg_ctx* c) {
+  if (!c->sw.stats_spin) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return;
+  }
+  stats_words_alloc(c);
+  const unsigned seq = next_seq(c->stats_seq);
+  hipLaunchKernelGGL(word_kernel, dim3(1), dim3(64), 0, c->stream, c->h_stats_word, seq);
+  HIP_TRY(hipGetLastError());
+  wait_words(c, c->h_stats_word, 1, seq);
+}
+
 // The stats (q_max, loss) of the work queued so far, synchronously.
 static void read_stats(ddpg_ctx* c, float st[2]) {
   if (c->sw.stats_spin) {
-    if (!c->h_stats_word) {
-      HIP_TRY(hipHostMalloc(&c->h_stats_word, 4 * sizeof(unsigned), hipHostMallocCoherent));
-      memset(c->h_stats_word, 0, 4 * sizeof(unsigned));
-    }
+    stats_words_alloc(c);
     const unsigned seq = next_seq(c->stats_seq);
     float* out = reinterpret_cast<float*>(c->h_stats_word + 1);
     hipLaunchKernelGGL(stats_out_kernel, dim3(1), dim3(64), 0, c->stream, c->dstats, out,
