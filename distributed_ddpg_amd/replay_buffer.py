@@ -80,6 +80,11 @@ class ReplayBuffer:
         w["s_np"][:] = np.ravel(s)
         w["s2_np"][:] = np.ravel(s2)
         w["a_np"][:] = np.ravel(a)
+        if not np.isscalar(r):  # a one-element array or list (some envs' rewards)
+            rr = np.ravel(r)
+            if rr.size != 1:
+                raise ValueError("reward must be a scalar, got %d values" % rr.size)
+            r = rr[0]
         w["r_np"][0] = r
         w["t"][0] = 1 if t else 0
         self._err(w["fn"](self._rb, w["s"], w["a"], w["r"], w["t"], w["s2"], 1))

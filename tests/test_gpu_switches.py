@@ -663,9 +663,16 @@ def test_ring_args_bitwise(dd, O, monkeypatch, f64):
         fl = FusedLearner(sess, rb, B)
         st = []
         for i in range(n):
-            rb.add(rows[0][i], rows[1][i], rows[2][i], rows[3][i], rows[4][i])
+            # the reward as a scalar, or as a one-element array (some envs)
+            r_i = rows[2][i] if i % 2 else np.array([rows[2][i]])
+            rb.add(rows[0][i], rows[1][i], r_i, rows[3][i], rows[4][i])
             if i >= B and i % 3 == 0:
                 st.append(fl.step(stats=i % 2 == 0))
+        with pytest.raises(ValueError):
+            rb.add(rows[0][0][:-1], rows[1][0], 0.0, False, rows[4][0])  # short state
+        with pytest.raises(ValueError):
+            rb.add(rows[0][0], rows[1][0], np.zeros(2), False, rows[4][0])  # two rewards
+        assert rb.size() == 500
         s_b, a_b, r_b, t_b, s2_b, pos = rb.sample_batch(64, return_indices=True)
         ins = (n - rb.size()) + np.asarray(pos)  # insertion index of each sampled row
         assert np.array_equal(s_b, rows[0][ins]) and np.array_equal(s2_b, rows[4][ins])
